@@ -1,0 +1,185 @@
+/* rdmi.h — C ABI of librdmi.so, the MI355X (gfx950) HIP kernels of RollingDepth's
+ * snippet-denoise hot path.
+ *
+ * The reference (yizuo417/RollingDepth) has no native code and no FFI: its hot path is implicit
+ * PyTorch library kernels issued from Python.  Each entry point below
+ * replaces one such implicit op (or a fused group of them) and names the reference call site it
+ * stands in for.  The Python host package `rollingdepth_amd` binds these through ctypes
+ * (INTEGRATION.md shows the binding a maintainer of the reference would add).
+ *
+ * Conventions:
+ *  - plain pointers (device memory owned by the caller), sizes and strides in ELEMENTS, and a
+ *    hipStream_t passed as `void*` (0 = the null stream);
+ *  - activations are NHWC / token-major [B, S, C]; f16 storage with f32 accumulation unless a
+ *    parameter says otherwise; norm affine parameters and biases are f32;
+ *  - every call returns 0 or an error code (RDMI_E_* for bad arguments, else the hipError_t of
+ *    the launch); rdmi_last_error() returns a thread-local message; nothing synchronises the
+ *    device, allocates, frees, or retains a pointer after return, so every call is graph-capturable.
+ */
+#ifndef RDMI_H
+#define RDMI_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RDMI_OK 0
+#define RDMI_E_ARG 1001         /* bad shape / stride / null pointer */
+#define RDMI_E_ALIGN 1002       /* pointer or leading dimension not 16-byte aligned */
+#define RDMI_E_UNSUPPORTED 1003 /* configuration this build does not implement */
+
+#define RDMI_EPI_NONE 0
+#define RDMI_EPI_GEGLU 1 /* out[:, n] = (h + b_h) * gelu_erf(g + b_g), weights row-interleaved */
+
+/* ---------------------------------------------------------------------------------------
+ * Library
+ */
+const char* rdmi_last_error(void);
+int rdmi_version(void);
+
+/* ---------------------------------------------------------------------------------------
+ * GEMM (Linear layers): C[b] = alpha * A[b] · W[b]ᵀ (+ bias[n]) (+ rowbias[m / rows_per_group][n])
+ *                                                     (+ residual[b][m][n])
+ * A [M, K] f16 (lda), W [N, K] f16 (ldw ≥ K), K % 8 == 0, C f16 or f32 (ldc).
+ * Replaces torch.nn.Linear / F.linear in Attention.to_q/k/v/to_out
+ * (diffusers/models/attention_processor.py:2226-2261), FeedForward/GEGLU
+ * (diffusers/models/attention.py:1116, activations.py:113-123), Transformer2DModel.proj_in/out
+ * (transformers/transformer_2d.py:485-533) and TimestepEmbedding (embeddings.py:543).
+ */
+typedef struct rdmi_gemm_args {
+  const void* A; long lda; long strideA;
+  const void* W; long ldw; long strideW;
+  void* C; long ldc; long strideC; int c_f32;
+  const float* bias;
+  const void* residual; long ldr; long strideR;
+  const float* rowbias; int rows_per_group; long rowbias_ld;
+  float alpha;
+  int M, N, K, batch;
+  int epilogue;
+} rdmi_gemm_args;
+int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Convolution as implicit GEMM on NHWC f16 (MFMA 16x16x32 f16, f32 accumulate).
+ * y[b, ho, wo, co] = alpha * Σ w[co, dy, dx, ci] x[b, ho*s - pt + dy, wo*s - pl + dx, ci]
+ *                    (+ bias[co]) (+ rowbias[b][co]) (+ residual[b, ho, wo, co])
+ * `upsample`=1 reads x through a nearest ×2 upsample (Upsample2D, upsampling.py:141-190) without
+ * materialising it.  Cin % 8 == 0 (pad channels); w is [Cout][kh][kw][Cin] padded to Kp % 32 == 0.
+ * Replaces the cuDNN conv2d of ResnetBlock2D.conv1/conv2/conv_shortcut (resnet.py:320-373),
+ * Downsample2D (downsampling.py:132-148, including the VAE's F.pad(0,1,0,1) via pad_top/left=0
+ * with the extra row/column read as zero), Upsample2D.conv, conv_in/conv_out of the UNet and VAE.
+ */
+typedef struct rdmi_conv_args {
+  const void* x; const void* w; void* y;
+  const float* bias; const void* residual; const float* rowbias;
+  int B, H, W, Cin, Cout, kh, kw, stride, pad_top, pad_left, upsample, Ho, Wo, Kp;
+  long y_ld; long res_ld; float alpha;
+} rdmi_conv_args;
+int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * GroupNorm on NHWC f16: statistics then apply (optionally fused SiLU).
+ * Replaces F.group_norm (+ SiLU) of ResnetBlock2D.norm1/norm2 (resnet.py:326,351),
+ * Transformer2DModel.norm (transformer_2d.py:175-177), conv_norm_out of UNet/VAE, and the VAE
+ * mid-block Attention.group_norm (attention_processor.py:2221-2222).
+ * stats: mean_rstd[b*G + g] = {mean, rstd}; workspace ≥ rdmi_groupnorm_workspace(B, G) floats.
+ */
+long rdmi_groupnorm_workspace(int B, int G);
+int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G, float eps,
+                         float* mean_rstd, float* workspace, void* stream);
+int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G,
+                         const float* mean_rstd, const float* gamma, const float* beta, int silu,
+                         void* stream);
+
+/* LayerNorm over the last dim (BasicTransformerBlock.norm1/2/3, attention.py:445,495,522). */
+int rdmi_layernorm(const void* x, void* y, long M, int C, const float* gamma, const float* beta,
+                   float eps, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Fused multi-head attention forward, softmax(q kᵀ · scale) v, non-causal, no mask, D = 64.
+ * Token-major q/k/v/o with row strides (ld*) and batch strides (bs*), head h at column h*D.
+ * With the num_view fold done by the caller's strides (one "batch" = one snippet of n frames,
+ * S = n·h·w), this is the cross-frame self-attention of the modified AttnProcessor2_0
+ * (attention_processor.py:2208-2266) / XFormersAttnProcessor (:1989-2050).
+ */
+int rdmi_attention_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
+                       int Sk, int D, long q_ld, long k_ld, long v_ld, long o_ld, long q_bs,
+                       long k_bs, long v_bs, long o_bs, float scale, void* stream);
+
+/* Attention against a short key set (L ≤ 16 keys, e.g. the 2-token empty-text context of the
+ * UNet cross-attention attn2, attention.py:508-516); k/v [Bkv][L][H*D] contiguous, Bkv ∈ {1, B}. */
+int rdmi_attention_smallkv(const void* q, const void* k, const void* v, void* o, int B, int H,
+                           int Sq, int L, int D, long q_ld, long o_ld, long q_bs, long o_bs,
+                           long kv_bs, float scale, void* stream);
+
+/* Row softmax: p[r, :] = softmax(scale * s[r, :]) (f32 in, f16 out).  Used with two rdmi_gemm
+ * calls for the single-head d=C VAE mid-block attention (unet_2d_blocks.py:680-697). */
+int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, float scale, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Layout / elementwise helpers (f16 NHWC unless stated)
+ */
+/* NCHW (f32 if x_f32 else f16) → NHWC f16 with channel padding to Cpad (zeros), y = x*scale */
+int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int B, int C, int H, int W, int Cpad,
+                      float scale, void* stream);
+/* NHWC f16 (ld = channel stride) → NCHW f32, first C channels, y = x*scale + shift */
+int rdmi_nhwc_to_nchw_f32(const void* x, long ld, float* y, int B, int C, int H, int W,
+                          float scale, float shift, void* stream);
+/* y[p, 0:Ca] = a[p, :], y[p, Ca:Ca+Cb] = b[p, :]  (torch.cat dim=1 of CrossAttn/UpBlock skips) */
+int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, void* stream);
+/* 2-D transpose per batch: dst[b][c][r] = src[b][r][c] (f16) */
+int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, long src_ld,
+                   long dst_ld, void* stream);
+/* Build the 8-channel UNet input of single_step (rollingdepth_pipeline.py:646-651):
+ * out[i, p, 0:4] = rgb[frame_idx[i], p, 0:4], out[i, p, 4:8] = depth[dsel(i), p, 0:4]
+ * (depth_ld: frame stride of `depth` in elements; depth_bcast=1 uses depth frame 0 for all). */
+int rdmi_gather_unet_input(const void* rgb, long rgb_frame_ld, const void* depth,
+                           long depth_frame_ld, int depth_bcast, const int* frame_idx, int count,
+                           long HW, void* out, void* stream);
+/* DDIM step (eta = 0) as the affine map the 1-step scheduler reduces to
+ * (scheduling_ddim.py:402-448): y = (ca·x + cb·e) * out_scale; x, e: [P] with strides, y [P, ld_y]
+ * channels 0..C-1, channels C..Cpad-1 of y zeroed. */
+int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* y, long ld_y,
+                      long P, int C, int Cpad, float ca, float cb, float out_scale, void* stream);
+/* Global min/max of an f16 or f32 buffer → minmax[2] f32 (workspace ≥ 2*1024 floats)
+ * (the `min([snippet.min() ...])` of depth_aligner.py:78 and the min/max of :316-317). */
+int rdmi_minmax(const void* x, int x_f32, long n, float* minmax, float* workspace, void* stream);
+/* In place: x = (x - mn) / (mx - mn) * 2 - 1 with mn,mx read from device (re-normalise, :316-318) */
+int rdmi_renormalize_f32(float* x, long n, const float* minmax, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * DepthAligner (rollingdepth/depth_aligner.py) — co-alignment of dilated snippets.
+ * Snippet layout: one f32 buffer per dilation, x_d [n_d][w][P] (border-cropped, stride-subsampled,
+ * min-shifted; depth_aligner.py:78-92).  Parameters s_d, t_d are f32 [n_d].
+ */
+typedef struct rdmi_aligner_args {
+  int n_dil;                 /* number of dilations (≤ 8) */
+  const float* x[8];         /* subsampled snippets per dilation [n_d][w][P] */
+  float* s[8]; float* t[8];  /* scales / translations [n_d] (in: init, out: result) */
+  int n[8]; int stride[8];   /* snippets per dilation, frame stride (dilation) */
+  int w;                     /* snippet length (all dilations) */
+  int seq_len; long P;
+  float lr, beta1, beta2, eps, lmda2, lmda3, depth_w, loss_scale;
+  int iters;
+  float* history;            /* [iters][3] (loss, min summ, max summ) or NULL */
+  float* workspace;          /* ≥ rdmi_aligner_workspace(...) floats */
+} rdmi_aligner_args;
+long rdmi_aligner_workspace(const rdmi_aligner_args* a);
+/* Adam loop of DepthAligner.optimize (:123-229) fully on device, no host sync. */
+int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream);
+/* Border crop + stride subsample + min shift of one dilation's decoded snippets
+ * x [n][w][H][W] (f16/f32) → out [n][w][P] f32 with out = dtype(x - shift[0]) (:78-92). */
+int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int H, int W, int border,
+                         int factor, const float* shift, float* out, void* stream);
+/* merge_scaled_triplets (:231-262): full-resolution snippets per dilation xf_d [n_d][w][HW]
+ * (f16 or f32 per x_f32; the min shift read from shift[0] is applied first, in that dtype),
+ * s/t f32 → out [seq_len][HW] f32 (s·x+t rounded through the snippet dtype exactly where the
+ * reference computes in it; the per-frame mean is accumulated in f32). */
+int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                       const float* const* t, const int* n, const int* stride, int w, int seq_len,
+                       long HW, const float* shift, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RDMI_H */

@@ -1,0 +1,70 @@
+"""Build librdmi.so (gfx950) in-tree with hipcc.
+
+    python -m rollingdepth_amd._build [--force]
+
+Each csrc/*.hip / *.cpp is compiled to an object under build/ (incremental on mtimes of the
+source, csrc/common.h and include/rdmi.h) and linked into rollingdepth_amd/_lib/librdmi.so, which
+travels to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIB_DIR, "librdmi.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
+         "-Wno-unused-result"]
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+
+
+def _deps_mtime():
+    return max(os.path.getmtime(os.path.join(CSRC, "common.h")),
+               os.path.getmtime(os.path.join(ROOT, "include", "rdmi.h")))
+
+
+def _compile(src, force):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), _deps_mtime()):
+        return obj, None
+    lang = ["-x", "hip"] if src.endswith(".hip") else []
+    cmd = [HIPCC, *FLAGS, "-c", *lang, src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return obj, None
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        results = list(ex.map(lambda s: _compile(s, force), srcs))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("librdmi build failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in results]
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"librdmi link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print(LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,68 @@
+"""DepthAligner — drop-in for rollingdepth/depth_aligner.py:29-262 running on librdmi.
+
+Same constructor keywords, same `run(snippet_ls, dilations)` contract and return value
+(merged [N,1,H,W] in the snippets' dtype, scales / translations as [n_d,1,1] f32, loss history
+as a list of (loss, min(summ), max(summ)) tuples).  The 2000-iteration Adam loop is enqueued
+entirely on the device (aligner.hip); the only host sync is reading the loss history at the end.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from . import kernels as K
+
+
+class DepthAligner:
+    def __init__(self, device: torch.device, factor: int = 10, lmda: float = 1e-1, lmda2: float = 1e-1,
+                 lmda3: float = 1e1, lr: float = 1e-3, num_iterations: int = 2000, border: int = 2,
+                 verbose: bool = False, depth_loss_weight: float = 1.0, loss_scale=1.0):
+        self.factor = factor
+        self.lmda = lmda  # kept for signature parity; unused by the reference loss too
+        self.lr = lr
+        self.num_iterations = num_iterations
+        self.border = border
+        self.verbose = verbose
+        self.device = device
+        self.lmda2 = lmda2
+        self.depth_loss_weight = depth_loss_weight
+        self.loss_scale = loss_scale
+        self.lmda3 = lmda3
+
+    def create_triplet_indices(self, sequence_length: int, gap: int, window_size: int) -> torch.Tensor:
+        """depth_aligner.py:57-66."""
+        gap += 1
+        return torch.tensor([[i + j * gap for j in range(window_size)]
+                             for i in range(sequence_length - (window_size - 1) * gap)])
+
+    def run(self, snippet_ls: List[torch.Tensor], dilations: List[int]):
+        dev = torch.device(self.device)
+        snippet_ls = [s.to(dev) for s in snippet_ls]
+        lengths = [s.shape[1] for s in snippet_ls]
+        if len(set(lengths)) != 1:
+            raise NotImplementedError("DepthAligner (librdmi): all dilations must share one snippet length")
+        w = lengths[0]
+        gaps = [d - 1 for d in dilations]
+        seq_len = len(snippet_ls[0]) + (w - 1) * gaps[0] + (w - 1)
+        for s, g in zip(snippet_ls, gaps):
+            expect = seq_len - (w - 1) * (g + 1)
+            if s.shape[0] != expect:
+                raise ValueError(f"snippet count {s.shape[0]} != {expect} for dilation {g + 1}")
+        dtype = snippet_ls[0].dtype
+        flat = [s.reshape(s.shape[0], w, s.shape[-2], s.shape[-1]).contiguous() for s in snippet_ls]
+        # global min over every snippet (depth_aligner.py:78)
+        mins = torch.stack([K.minmax(s) for s in flat]).reshape(-1)
+        shift = K.minmax(mins)
+        xs = [K.aligner_prepare(s, shift, self.border, self.factor) for s in flat]
+        scales = [torch.ones(x.shape[0], dtype=torch.float32, device=dev) for x in xs]
+        trans = [torch.zeros(x.shape[0], dtype=torch.float32, device=dev) for x in xs]
+        hist = torch.zeros((max(self.num_iterations, 1), 3), dtype=torch.float32, device=dev)
+        strides = [g + 1 for g in gaps]
+        ws = K.aligner_optimize(xs, scales, trans, strides, seq_len, self.lr, (0.5, 0.9), 1e-8, self.lmda2,
+                                self.lmda3, self.depth_loss_weight, self.loss_scale, self.num_iterations, hist)
+        merged = K.aligner_merge(flat, scales, trans, strides, seq_len, shift)
+        merged = merged.to(dtype)[:, None]
+        loss_ls = [tuple(r) for r in hist[: self.num_iterations].tolist()]
+        del ws
+        return (merged, [s.view(-1, 1, 1) for s in scales], [t.view(-1, 1, 1) for t in trans], loss_ls)

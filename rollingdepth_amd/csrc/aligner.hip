@@ -1,0 +1,381 @@
+// DepthAligner on device (rollingdepth/depth_aligner.py).
+//
+// The reference runs 2000 Adam iterations of per-snippet scale/shift optimisation through
+// autograd, with three host syncs per iteration (loss.item(), summ.min/max, :213).  Here one
+// iteration is three kernels with no host involvement:
+//   frame_stats  — per frame f and subsampled pixel p, the mean over every covering (dilation,
+//                  slot) of A = x·s + t and of 1/clip(A, 1e-3) (the M / M_depth / B scatter and
+//                  the .sum(0)/B.sum(0) of :169-191, summed in the reference's row order), plus
+//                  the per-frame L1 scales mean|T| (:197-198) and min/max for the loss history;
+//   snippet_grad — per snippet the analytic gradient of the L1 + inverse-depth L1 loss
+//                  (:200-203) w.r.t. its s and t (sign(A−T)/scale, the clip mask A ≥ 1e-3, the
+//                  −1/clip² of pow(−1)), reduced in f64 in a fixed order (deterministic);
+//   adam         — soft constraints λ2·mean(relu(1−s)²) + λ3·mean(t²) (:205-209) and
+//                  torch.optim.Adam's single-tensor update in its exact f32 op order (lerp,
+//                  mul+addcmul, sqrt/bc2_sqrt + eps, addcdiv), loss history row.
+// merge        — merge_scaled_triplets (:231-262): per frame the mean over all covering slots of
+//                s·x+t, rounded through the snippet dtype where the reference computes in it.
+#pragma clang fp contract(off)
+#include "common.h"
+
+namespace {
+
+constexpr int MAXD = 8;
+
+struct AlP {
+  const float* x[MAXD];
+  float* s[MAXD];
+  float* t[MAXD];
+  int n[MAXD], stride[MAXD], off[MAXD];  // off: first global snippet index of dilation d
+  int nd, w, N;
+  long P;
+  float lr, b1, b2, eps, lmda2, lmda3, dw, ls;
+  // workspace views
+  float *T, *Td, *scale, *scaled, *fmin, *fmax;
+  double *gs, *gt, *l1, *l2;
+  float *m, *v;  // Adam moments [2*Ntot] (s then t)
+  float* hist;
+  int ntot;
+};
+
+__device__ __forceinline__ float mulrn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float addrn(float a, float b) { return __fadd_rn(a, b); }
+
+template <int BS>
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  for (int i = 0; i < BS / 64; ++i) r += sh[i];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void frame_stats(AlP p) {
+  const int f = blockIdx.x;
+  __shared__ double sh[8];
+  double sa = 0.0, sd = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+  for (long px = threadIdx.x; px < p.P; px += 256) {
+    float sum = 0.f, sumd = 0.f;
+    int cnt = 0;
+    for (int d = 0; d < p.nd; ++d) {
+      for (int j = 0; j < p.w; ++j) {
+        int k = f - j * p.stride[d];
+        if (k < 0 || k >= p.n[d]) continue;
+        float a = addrn(mulrn(p.x[d][((long)k * p.w + j) * p.P + px], p.s[d][k]), p.t[d][k]);
+        float ac = fmaxf(a, 1e-3f);
+        sum = addrn(sum, a);
+        sumd = addrn(sumd, 1.0f / ac);
+        ++cnt;
+      }
+    }
+    float T = 0.f, Td = 0.f;
+    if (cnt) {
+      T = sum / (float)cnt;
+      Td = sumd / (float)cnt;
+    }
+    p.T[(long)f * p.P + px] = T;
+    p.Td[(long)f * p.P + px] = Td;
+    sa += fabs((double)T);
+    sd += fabs((double)Td);
+    mn = fminf(mn, T);
+    mx = fmaxf(mx, T);
+  }
+  double A = block_sum_d<256>(sa, sh);
+  double D = block_sum_d<256>(sd, sh);
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  __shared__ float r[2][4];
+  if ((threadIdx.x & 63) == 0) {
+    r[0][threadIdx.x >> 6] = mn;
+    r[1][threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    p.scale[f] = (float)(A / (double)p.P);
+    p.scaled[f] = (float)(D / (double)p.P);
+    p.fmin[f] = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
+    p.fmax[f] = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
+  }
+}
+
+__global__ __launch_bounds__(256) void snippet_grad(AlP p) {
+  const int gk = blockIdx.x;  // global snippet index
+  int d = 0;
+  while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
+  const int k = gk - p.off[d];
+  const float s = p.s[d][k], t = p.t[d][k];
+  const float* x = p.x[d] + (long)k * p.w * p.P;
+  double gs = 0.0, gt = 0.0, l1 = 0.0, l2 = 0.0;
+  for (int j = 0; j < p.w; ++j) {
+    const int f = k + j * p.stride[d];
+    const float isc = 1.0f / p.scale[f], iscd = 1.0f / p.scaled[f];
+    const float* Tf = p.T + (long)f * p.P;
+    const float* Tdf = p.Td + (long)f * p.P;
+    for (long px = threadIdx.x; px < p.P; px += 256) {
+      float xv = x[(long)j * p.P + px];
+      float a = addrn(mulrn(xv, s), t);
+      float z = a - Tf[px];
+      float ac = fmaxf(a, 1e-3f);
+      float ad = 1.0f / ac;
+      float zd = ad - Tdf[px];
+      float g1 = (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) * isc;
+      float g2 = 0.f;
+      if (a >= 1e-3f) g2 = (zd > 0.f ? 1.f : (zd < 0.f ? -1.f : 0.f)) * iscd * (-1.0f / (ac * ac));
+      double g = (double)g1 + (double)p.dw * (double)g2;
+      gs += g * (double)xv;
+      gt += g;
+      l1 += fabs((double)z) * (double)isc;
+      l2 += fabs((double)zd) * (double)iscd;
+    }
+  }
+  __shared__ double sh[8];
+  gs = block_sum_d<256>(gs, sh);
+  gt = block_sum_d<256>(gt, sh);
+  l1 = block_sum_d<256>(l1, sh);
+  l2 = block_sum_d<256>(l2, sh);
+  if (threadIdx.x == 0) {
+    p.gs[gk] = gs;
+    p.gt[gk] = gt;
+    p.l1[gk] = l1;
+    p.l2[gk] = l2;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) {
+  __shared__ double sh[8];
+  // loss history (uses the parameters BEFORE this update, like the closure's loss)
+  double L1 = 0.0, L2 = 0.0, soft = 0.0;
+  for (int i = threadIdx.x; i < p.ntot; i += 256) {
+    L1 += p.l1[i];
+    L2 += p.l2[i];
+  }
+  L1 = block_sum_d<256>(L1, sh);
+  L2 = block_sum_d<256>(L2, sh);
+  for (int d = 0; d < p.nd; ++d) {
+    double a = 0.0, b = 0.0;
+    for (int k = threadIdx.x; k < p.n[d]; k += 256) {
+      float r = fmaxf(0.f, 1.f - p.s[d][k]);
+      a += (double)r * r;
+      b += (double)p.t[d][k] * p.t[d][k];
+    }
+    a = block_sum_d<256>(a, sh);
+    b = block_sum_d<256>(b, sh);
+    soft += p.lmda2 * a / p.n[d] + p.lmda3 * b / p.n[d];
+  }
+  if (p.hist && threadIdx.x == 0) {
+    float mn = INFINITY, mx = -INFINITY;
+    for (int f = 0; f < p.N; ++f) {
+      mn = fminf(mn, p.fmin[f]);
+      mx = fmaxf(mx, p.fmax[f]);
+    }
+    float* h = p.hist + 3L * (step - 1);
+    h[0] = (float)(p.ls * (L1 / denom + p.dw * L2 / denom) + soft);
+    h[1] = mn;
+    h[2] = mx;
+  }
+  __syncthreads();
+  const double bc1 = 1.0 - pow((double)p.b1, (double)step);
+  const double bc2 = 1.0 - pow((double)p.b2, (double)step);
+  const float step_size = (float)(p.lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  const float lw = 1.0f - p.b1;   // lerp weight (1 - beta1)
+  const float vw = 1.0f - p.b2;   // addcmul value (1 - beta2)
+  const float gscale = (float)(p.ls / denom);
+  for (int i = threadIdx.x; i < 2 * p.ntot; i += 256) {
+    const bool is_t = i >= p.ntot;
+    const int gk = is_t ? i - p.ntot : i;
+    int d = 0;
+    while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
+    const int k = gk - p.off[d];
+    float* prm = is_t ? &p.t[d][k] : &p.s[d][k];
+    const float pv = *prm;
+    float g = (float)((is_t ? p.gt[gk] : p.gs[gk]) * (double)gscale);
+    const float nd = (float)p.n[d];
+    if (!is_t) {
+      float r = fmaxf(0.f, 1.f - pv);
+      g = addrn(g, mulrn(mulrn(mulrn(p.lmda2, 2.0f), r), -1.0f) / nd);
+    } else {
+      g = addrn(g, mulrn(mulrn(p.lmda3, 2.0f), pv) / nd);
+    }
+    float m = p.m[i], v = p.v[i];
+    const float diff = g - m;
+    m = (lw < 0.5f) ? addrn(m, mulrn(lw, diff)) : g - mulrn(diff, 1.0f - lw);
+    v = addrn(mulrn(v, p.b2), mulrn(mulrn(vw, g), g));
+    const float den = addrn(sqrtf(v) / bc2s, p.eps);
+    *prm = addrn(pv, mulrn(-step_size, m) / den);
+    p.m[i] = m;
+    p.v[i] = v;
+  }
+}
+
+__global__ void zero_f32(float* x, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] = 0.f;
+}
+
+struct MergeP {
+  const void* x[MAXD];
+  const float* s[MAXD];
+  const float* t[MAXD];
+  int n[MAXD], stride[MAXD];
+  int nd, w, xf32;
+  long HW;
+  const float* shift;
+  float* out;
+};
+
+__global__ void merge_k(MergeP p) {
+  const int f = blockIdx.y;
+  const float sh = p.shift ? p.shift[0] : 0.f;
+  for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
+    float sum = 0.f;
+    int cnt = 0;
+    for (int d = 0; d < p.nd; ++d) {
+      for (int j = p.w - 1; j >= 0; --j) {  // boolean-mask order over [n_d, w]: k ascending
+        int k = f - j * p.stride[d];
+        if (k < 0 || k >= p.n[d]) continue;
+        long off = ((long)k * p.w + j) * p.HW + px;
+        float a;
+        if (p.xf32) {
+          float xs = ((const float*)p.x[d])[off] - sh;
+          a = addrn(mulrn(xs, p.s[d][k]), p.t[d][k]);
+        } else {
+          f16 xs = (f16)((float)((const f16*)p.x[d])[off] - sh);
+          f16 sc = (f16)p.s[d][k], tr = (f16)p.t[d][k];
+          f16 prod = (f16)((float)xs * (float)sc);
+          a = (float)(f16)((float)prod + (float)tr);
+        }
+        sum = addrn(sum, a);
+        ++cnt;
+      }
+    }
+    p.out[(long)f * p.HW + px] = cnt ? sum / (float)cnt : 0.f;
+  }
+}
+
+struct PrepP {
+  const void* x;
+  int xf32;
+  int n, w, H, W, border, factor, Hs, Ws;
+  const float* shift;
+  float* out;
+};
+
+__global__ void prepare_k(PrepP p) {
+  const long P = (long)p.Hs * p.Ws;
+  const long total = (long)p.n * p.w * P;
+  const float sh = p.shift[0];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long img = i / P, q = i - img * P;
+    int ys = (int)(q / p.Ws), xs = (int)(q - (long)ys * p.Ws);
+    long src = img * p.H * p.W + (long)(p.border + ys * p.factor) * p.W + (p.border + xs * p.factor);
+    float v;
+    if (p.xf32)
+      v = ((const float*)p.x)[src] - sh;
+    else
+      v = (float)(f16)((float)((const f16*)p.x)[src] - sh);
+    p.out[i] = v;
+  }
+}
+
+long ws_floats(int N, long P, int ntot) {
+  // T, Td (N*P each), scale, scaled, fmin, fmax (N each), 4 double arrays (ntot each), m, v (2*ntot each)
+  return 2L * N * P + 4L * N + 8L * ntot + 4L * ntot + 64;
+}
+
+}  // namespace
+
+extern "C" long rdmi_aligner_workspace(const rdmi_aligner_args* a) {
+  int ntot = 0;
+  for (int d = 0; d < a->n_dil; ++d) ntot += a->n[d];
+  return ws_floats(a->seq_len, a->P, ntot);
+}
+
+extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
+  RDMI_REQUIRE(a && a->workspace && a->n_dil >= 1 && a->n_dil <= MAXD && a->w >= 1 && a->P > 0 && a->seq_len > 0,
+               RDMI_E_ARG, "aligner_optimize: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  AlP p{};
+  p.nd = a->n_dil;
+  p.w = a->w;
+  p.N = a->seq_len;
+  p.P = a->P;
+  int ntot = 0;
+  for (int d = 0; d < p.nd; ++d) {
+    RDMI_REQUIRE(a->x[d] && a->s[d] && a->t[d] && a->n[d] > 0, RDMI_E_ARG, "aligner_optimize: dilation %d", d);
+    p.x[d] = a->x[d];
+    p.s[d] = a->s[d];
+    p.t[d] = a->t[d];
+    p.n[d] = a->n[d];
+    p.stride[d] = a->stride[d];
+    p.off[d] = ntot;
+    ntot += a->n[d];
+  }
+  p.ntot = ntot;
+  p.lr = a->lr; p.b1 = a->beta1; p.b2 = a->beta2; p.eps = a->eps;
+  p.lmda2 = a->lmda2; p.lmda3 = a->lmda3; p.dw = a->depth_w; p.ls = a->loss_scale;
+  float* w = a->workspace;
+  RDMI_REQUIRE(((uintptr_t)w & 7) == 0, RDMI_E_ALIGN, "aligner: workspace must be 8-byte aligned");
+  double* dw = (double*)w;
+  p.gs = dw; p.gt = dw + ntot; p.l1 = dw + 2 * ntot; p.l2 = dw + 3 * ntot;
+  float* fw = (float*)(dw + 4 * ntot);
+  p.T = fw; fw += (long)p.N * p.P;
+  p.Td = fw; fw += (long)p.N * p.P;
+  p.scale = fw; fw += p.N;
+  p.scaled = fw; fw += p.N;
+  p.fmin = fw; fw += p.N;
+  p.fmax = fw; fw += p.N;
+  p.m = fw; fw += 2 * ntot;
+  p.v = fw; fw += 2 * ntot;
+  p.hist = a->history;
+  int W = 0;
+  for (int d = 0; d < p.nd; ++d) W += p.w;
+  const double denom = (double)W * p.N * (double)p.P;  // numel of the [Σw, N, P] loss tensor
+  hipLaunchKernelGGL(zero_f32, dim3(16), dim3(256), 0, st, p.m, 4L * ntot);
+  int rc = rdmi::check_launch("aligner_zero");
+  if (rc) return rc;
+  for (int it = 1; it <= a->iters; ++it) {
+    hipLaunchKernelGGL(frame_stats, dim3(p.N), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(snippet_grad, dim3(ntot), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(adam_step, dim3(1), dim3(256), 0, st, p, it, denom);
+    rc = rdmi::check_launch("aligner_iteration");
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+extern "C" int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int H, int W, int border, int factor,
+                                    const float* shift, float* out, void* stream) {
+  RDMI_REQUIRE(x && shift && out && H > 2 * border && W > 2 * border && factor > 0, RDMI_E_ARG,
+               "aligner_prepare: bad args");
+  PrepP p{x, x_f32, n, w, H, W, border, factor, (H - 2 * border + factor - 1) / factor,
+          (W - 2 * border + factor - 1) / factor, shift, out};
+  long total = (long)n * w * p.Hs * p.Ws;
+  long g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(prepare_k, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, p);
+  return rdmi::check_launch("aligner_prepare");
+}
+
+extern "C" int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                                  const float* const* t, const int* n, const int* stride, int w, int seq_len, long HW,
+                                  const float* shift, float* out, void* stream) {
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && out && HW > 0, RDMI_E_ARG, "aligner_merge: bad args");
+  MergeP p{};
+  for (int d = 0; d < n_dil; ++d) {
+    p.x[d] = xf[d];
+    p.s[d] = s[d];
+    p.t[d] = t[d];
+    p.n[d] = n[d];
+    p.stride[d] = stride[d];
+  }
+  p.nd = n_dil; p.w = w; p.xf32 = x_f32; p.HW = HW; p.shift = shift; p.out = out;
+  long gx = (HW + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(merge_k, dim3((unsigned)gx, seq_len), dim3(256), 0, (hipStream_t)stream, p);
+  return rdmi::check_launch("aligner_merge");
+}

@@ -1,0 +1,58 @@
+// Shared definitions for librdmi (RollingDepth snippet-denoise path on MI355X / gfx950).
+// Conventions (include/rdmi.h): every entry point returns 0 or an RDMI_E_* / hipError_t code,
+// never synchronises the device, never allocates, and records a thread-local message.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdarg.h>
+
+#include "../../include/rdmi.h"
+
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+namespace rdmi {
+
+void set_error(const char* fmt, ...);
+
+// Check a launch; returns 0 or the HIP error code (message recorded).
+int check_launch(const char* what);
+
+inline int div_up(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace rdmi
+
+#define RDMI_REQUIRE(cond, code, ...)       \
+  do {                                       \
+    if (!(cond)) {                           \
+      rdmi::set_error(__VA_ARGS__);          \
+      return (code);                         \
+    }                                        \
+  } while (0)
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}

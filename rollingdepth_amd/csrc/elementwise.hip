@@ -1,0 +1,220 @@
+// Layout conversion and small fused elementwise steps of the snippet path (all HBM-bound,
+// grid-stride, 16-B vectors where the channel count allows).
+#include "common.h"
+
+namespace {
+
+inline unsigned grid_for(long n, int per_block = 256) {
+  long g = (n + per_block - 1) / per_block;
+  if (g > 16384) g = 16384;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+__global__ void nchw_to_nhwc_k(const void* __restrict__ x, int x_f32, f16* __restrict__ y, int C, long HW, int Cpad,
+                               long n, float scale) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    long pix = i / Cpad;
+    int c = (int)(i - pix * Cpad);
+    long b = pix / HW, p = pix - b * HW;
+    float v = 0.f;
+    if (c < C) {
+      long src = (b * C + c) * HW + p;
+      v = x_f32 ? ((const float*)x)[src] : (float)((const f16*)x)[src];
+      v *= scale;
+    }
+    y[i] = (f16)v;
+  }
+}
+
+__global__ void nhwc_to_nchw_k(const f16* __restrict__ x, long ld, float* __restrict__ y, int C, long HW, long n,
+                               float scale, float shift) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    long bc = i / HW, p = i - bc * HW;
+    long b = bc / C;
+    int c = (int)(bc - b * C);
+    y[i] = (float)x[(b * HW + p) * ld + c] * scale + shift;
+  }
+}
+
+__global__ void concat_k(const f16* __restrict__ a, int Ca, const f16* __restrict__ b, int Cb, f16* __restrict__ y,
+                         long P) {
+  const int CV = (Ca + Cb) >> 3, AV = Ca >> 3, BVv = Cb >> 3;
+  long n = P * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    long p = i / CV;
+    int cv = (int)(i - p * CV);
+    f16x8 v = cv < AV ? ((const f16x8*)a)[p * AV + cv] : ((const f16x8*)b)[p * BVv + (cv - AV)];
+    ((f16x8*)y)[i] = v;
+  }
+}
+
+__global__ void transpose_k(const f16* __restrict__ src, f16* __restrict__ dst, long rows, long cols, long sld,
+                            long dld) {
+  __shared__ f16 tile[64][65];
+  const int b = blockIdx.z;
+  const long r0 = blockIdx.y * 64L, c0 = blockIdx.x * 64L;
+  src += (long)b * rows * sld;
+  dst += (long)b * cols * dld;
+  for (int i = threadIdx.y; i < 64; i += 4) {
+    long r = r0 + i, c = c0 + threadIdx.x;
+    if (r < rows && c < cols) tile[i][threadIdx.x] = src[r * sld + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 64; i += 4) {
+    long c = c0 + i, r = r0 + threadIdx.x;
+    if (r < rows && c < cols) dst[c * dld + r] = tile[threadIdx.x][i];
+  }
+}
+
+// out [count][HW][8]: rgb latent channels 0..3, depth latent 4..7
+__global__ void gather_unet_input_k(const f16* __restrict__ rgb, long rgb_ld, const f16* __restrict__ depth,
+                                    long depth_ld, int bcast, const int* __restrict__ fidx, int count, long HW,
+                                    f16* __restrict__ out) {
+  long n = (long)count * HW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    int s = (int)(i / HW);
+    long p = i - (long)s * HW;
+    int f = fidx[s];
+    const f16* r = rgb + (long)f * rgb_ld + p * 8;
+    const f16* d = depth + (bcast ? 0 : (long)f * depth_ld) + p * 8;
+    f16x8 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = r[e];
+      v[4 + e] = d[e];
+    }
+    ((f16x8*)out)[i] = v;
+  }
+}
+
+__global__ void ddim_combine_k(const f16* __restrict__ x, long ldx, const f16* __restrict__ e, long lde,
+                               f16* __restrict__ y, long ldy, long P, int C, int Cpad, float ca, float cb, float sc) {
+  long n = P * Cpad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    long p = i / Cpad;
+    int c = (int)(i - p * Cpad);
+    float v = 0.f;
+    if (c < C) v = (ca * (float)x[p * ldx + c] + cb * (float)e[p * lde + c]) * sc;
+    y[p * ldy + c] = (f16)v;
+  }
+}
+
+__global__ void minmax_partial(const void* __restrict__ x, int xf32, long n, float* __restrict__ part) {
+  float mn = INFINITY, mx = -INFINITY;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = xf32 ? ((const float*)x)[i] : (float)((const f16*)x)[i];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  __shared__ float r[2][4];
+  if ((threadIdx.x & 63) == 0) {
+    r[0][threadIdx.x >> 6] = mn;
+    r[1][threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
+    part[2 * blockIdx.x + 1] = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
+  }
+}
+
+__global__ void minmax_final(const float* __restrict__ part, int nb, float* __restrict__ out) {
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = threadIdx.x; i < nb; i += 64) {
+    mn = fminf(mn, part[2 * i]);
+    mx = fmaxf(mx, part[2 * i + 1]);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  if (threadIdx.x == 0) {
+    out[0] = mn;
+    out[1] = mx;
+  }
+}
+
+// reference order (rollingdepth_pipeline.py:316-318): d -= min; d /= max(d); d = d*2 - 1
+__global__ void renorm_k(float* __restrict__ x, long n, const float* __restrict__ mm) {
+  const float mn = mm[0];
+  const float rng = mm[1] - mn;  // max(d - min) == max - min exactly for the max element
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = x[i] - mn;
+    v = v / rng;
+    x[i] = v * 2.0f - 1.0f;
+  }
+}
+
+}  // namespace
+
+extern "C" int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int B, int C, int H, int W, int Cpad, float scale,
+                                 void* stream) {
+  RDMI_REQUIRE(x && y && Cpad >= C, RDMI_E_ARG, "nchw_to_nhwc: bad args");
+  long n = (long)B * H * W * Cpad;
+  hipLaunchKernelGGL(nchw_to_nhwc_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, x_f32, (f16*)y, C,
+                     (long)H * W, Cpad, n, scale);
+  return rdmi::check_launch("nchw_to_nhwc");
+}
+
+extern "C" int rdmi_nhwc_to_nchw_f32(const void* x, long ld, float* y, int B, int C, int H, int W, float scale,
+                                     float shift, void* stream) {
+  RDMI_REQUIRE(x && y && ld >= C, RDMI_E_ARG, "nhwc_to_nchw: bad args");
+  long n = (long)B * C * H * W;
+  hipLaunchKernelGGL(nhwc_to_nchw_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld, y, C,
+                     (long)H * W, n, scale, shift);
+  return rdmi::check_launch("nhwc_to_nchw");
+}
+
+extern "C" int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, void* stream) {
+  RDMI_REQUIRE(a && b && y && Ca % 8 == 0 && Cb % 8 == 0, RDMI_E_ALIGN, "concat: channels must be multiples of 8");
+  long n = P * ((Ca + Cb) / 8);
+  hipLaunchKernelGGL(concat_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)a, Ca, (const f16*)b,
+                     Cb, (f16*)y, P);
+  return rdmi::check_launch("concat");
+}
+
+extern "C" int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, long src_ld, long dst_ld,
+                              void* stream) {
+  RDMI_REQUIRE(src && dst && rows > 0 && cols > 0, RDMI_E_ARG, "transpose: bad args");
+  dim3 g(rdmi::div_up(cols, 64), rdmi::div_up(rows, 64), batch);
+  hipLaunchKernelGGL(transpose_k, g, dim3(64, 4), 0, (hipStream_t)stream, (const f16*)src, (f16*)dst, rows, cols,
+                     src_ld, dst_ld);
+  return rdmi::check_launch("transpose");
+}
+
+extern "C" int rdmi_gather_unet_input(const void* rgb, long rgb_frame_ld, const void* depth, long depth_frame_ld,
+                                      int depth_bcast, const int* frame_idx, int count, long HW, void* out,
+                                      void* stream) {
+  RDMI_REQUIRE(rgb && depth && frame_idx && out && count > 0, RDMI_E_ARG, "gather_unet_input: bad args");
+  long n = (long)count * HW;
+  hipLaunchKernelGGL(gather_unet_input_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)rgb,
+                     rgb_frame_ld, (const f16*)depth, depth_frame_ld, depth_bcast, frame_idx, count, HW, (f16*)out);
+  return rdmi::check_launch("gather_unet_input");
+}
+
+extern "C" int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* y, long ld_y, long P, int C,
+                                 int Cpad, float ca, float cb, float out_scale, void* stream) {
+  RDMI_REQUIRE(x && e && y && Cpad >= C, RDMI_E_ARG, "ddim_combine: bad args");
+  long n = P * Cpad;
+  hipLaunchKernelGGL(ddim_combine_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld_x,
+                     (const f16*)e, ld_e, (f16*)y, ld_y, P, C, Cpad, ca, cb, out_scale);
+  return rdmi::check_launch("ddim_combine");
+}
+
+extern "C" int rdmi_minmax(const void* x, int x_f32, long n, float* minmax, float* workspace, void* stream) {
+  RDMI_REQUIRE(x && minmax && workspace && n > 0, RDMI_E_ARG, "minmax: bad args");
+  unsigned g = grid_for(n);
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(minmax_partial, dim3(g), dim3(256), 0, (hipStream_t)stream, x, x_f32, n, workspace);
+  int rc = rdmi::check_launch("minmax_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(minmax_final, dim3(1), dim3(64), 0, (hipStream_t)stream, workspace, (int)g, minmax);
+  return rdmi::check_launch("minmax_final");
+}
+
+extern "C" int rdmi_renormalize_f32(float* x, long n, const float* minmax, void* stream) {
+  RDMI_REQUIRE(x && minmax && n > 0, RDMI_E_ARG, "renormalize: bad args");
+  hipLaunchKernelGGL(renorm_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, minmax);
+  return rdmi::check_launch("renormalize");
+}

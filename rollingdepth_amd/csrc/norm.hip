@@ -1,0 +1,222 @@
+// GroupNorm (stats + apply[+SiLU]) and LayerNorm on NHWC / token-major f16 activations.
+// All three are HBM-bound streaming passes: 16-B vector loads, f64 per-thread accumulation for
+// the GroupNorm moments (no E[x²]−E[x]² cancellation at 10⁵-element groups), and a fixed
+// reduction order so results are bitwise reproducible run to run.
+#include "common.h"
+
+namespace {
+
+constexpr int GN_THREADS = 256;
+constexpr int GN_MAX_SPLIT = 256;
+
+// partial[b][split][g][2] (double sums)
+__global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__ x, long HW, int C, int G,
+                                                         int split, double* __restrict__ part) {
+  const int CV = C >> 3;
+  const int b = blockIdx.y;
+  const int sp = blockIdx.x;
+  const long r0 = HW * sp / split, r1 = HW * (sp + 1) / split;
+  const int RL = CV >= GN_THREADS ? 1 : GN_THREADS / CV;
+  const int ncol = (CV + GN_THREADS - 1) / GN_THREADS;  // ≤ 2 (C ≤ 4096)
+  const int t = threadIdx.x;
+  __shared__ double red[GN_THREADS][2][8][2];  // [thread][colset][elem][sum,sumsq] = 64 KB
+  const int cpg = C / G;
+  const f16* xb = x + (long)b * HW * C;
+  for (int cs = 0; cs < 2; ++cs) {
+    double s[8], ss[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.0;
+    int cv, rl;
+    bool active;
+    if (CV >= GN_THREADS) {
+      cv = t + cs * GN_THREADS;
+      rl = 0;
+      active = cs < ncol && cv < CV;
+    } else {
+      cv = t % CV;
+      rl = t / CV;
+      active = cs == 0 && rl < RL;
+    }
+    if (active) {
+      for (long r = r0 + rl; r < r1; r += RL) {
+        f16x8 v = *(const f16x8*)(xb + r * C + cv * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          double f = (double)(float)v[e];
+          s[e] += f;
+          ss[e] += f * f;
+        }
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[t][cs][e][0] = s[e];
+      red[t][cs][e][1] = ss[e];
+    }
+  }
+  __syncthreads();
+  // one thread per group sums its (thread, element) entries in a fixed order
+  for (int g = t; g < G; g += GN_THREADS) {
+    double S = 0.0, SS = 0.0;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      int cvv = c >> 3, e = c & 7;
+      if (CV >= GN_THREADS) {
+        int tt = cvv % GN_THREADS, cs = cvv / GN_THREADS;
+        S += red[tt][cs][e][0];
+        SS += red[tt][cs][e][1];
+      } else {
+        for (int rl = 0; rl < RL; ++rl) {
+          int tt = rl * CV + cvv;
+          S += red[tt][0][e][0];
+          SS += red[tt][0][e][1];
+        }
+      }
+    }
+    double* o = part + (((long)b * split + sp) * G + g) * 2;
+    o[0] = S;
+    o[1] = SS;
+  }
+}
+
+__global__ void gn_finalize(const double* __restrict__ part, int B, int G, int split, double n, float eps,
+                            float* __restrict__ mean_rstd) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * G) return;
+  int b = i / G, g = i % G;
+  double S = 0.0, SS = 0.0;
+  for (int sp = 0; sp < split; ++sp) {
+    const double* o = part + (((long)b * split + sp) * G + g) * 2;
+    S += o[0];
+    SS += o[1];
+  }
+  double mean = S / n;
+  double var = SS / n - mean * mean;
+  if (var < 0) var = 0;
+  mean_rstd[2 * i] = (float)mean;
+  mean_rstd[2 * i + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+__global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* __restrict__ y, long HW, int C,
+                                                int G, long nvec, const float* __restrict__ mr,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                int silu) {
+  const int CV = C >> 3;
+  const int cpg = C / G;
+  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
+    long pix = v / CV;
+    int c0 = (int)(v - pix * CV) * 8;
+    int b = (int)(pix / HW);
+    f16x8 in = *(const f16x8*)(x + v * 8);
+    f16x8 out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int c = c0 + e;
+      int g = c / cpg;
+      float mean = mr[2 * (b * G + g)], rstd = mr[2 * (b * G + g) + 1];
+      float f = ((float)in[e] - mean) * rstd * gamma[c] + beta[c];
+      if (silu) f = silu_f(f);
+      out[e] = (f16)f;
+    }
+    *(f16x8*)(y + v * 8) = out;
+  }
+}
+
+// one wave per row; C ≤ 64*8*4 = 2048
+__global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f16* __restrict__ y, long M, int C,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int CV = C >> 3;
+  const f16* xr = x + row * C;
+  f16x8 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int cv = lane + 64 * i;
+    if (cv < CV) {
+      v[i] = *(const f16x8*)(xr + cv * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)v[i][e];
+    }
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int cv = lane + 64 * i;
+    if (cv < CV) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float d = (float)v[i][e] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int cv = lane + 64 * i;
+    if (cv < CV) {
+      f16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        int c = cv * 8 + e;
+        o[e] = (f16)(((float)v[i][e] - mean) * rstd * gamma[c] + beta[c]);
+      }
+      *(f16x8*)(y + row * C + cv * 8) = o;
+    }
+  }
+}
+
+int gn_split(int B, long HW) {
+  long s = (1024 + B - 1) / B;
+  long maxs = (HW + 31) / 32;
+  if (s > maxs) s = maxs;
+  if (s > GN_MAX_SPLIT) s = GN_MAX_SPLIT;
+  if (s < 1) s = 1;
+  return (int)s;
+}
+
+}  // namespace
+
+extern "C" long rdmi_groupnorm_workspace(int B, int G) { return (long)B * GN_MAX_SPLIT * G * 4; }
+
+extern "C" int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G, float eps, float* mean_rstd,
+                                    float* workspace, void* stream) {
+  RDMI_REQUIRE(x && mean_rstd && workspace, RDMI_E_ARG, "groupnorm_stats: null pointer");
+  RDMI_REQUIRE(C % 8 == 0 && G > 0 && C % G == 0 && C <= 4096 && B > 0 && HW > 0, RDMI_E_ARG,
+               "groupnorm_stats: bad C=%d G=%d", C, G);
+  RDMI_REQUIRE(((uintptr_t)workspace & 7) == 0, RDMI_E_ALIGN, "groupnorm_stats: workspace not 8-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  int split = gn_split(B, HW);
+  double* part = (double*)workspace;
+  hipLaunchKernelGGL(gn_partial, dim3(split, B), dim3(GN_THREADS), 0, s, (const f16*)x, HW, C, G, split, part);
+  int rc = rdmi::check_launch("groupnorm_partial");
+  if (rc) return rc;
+  hipLaunchKernelGGL(gn_finalize, dim3(rdmi::div_up(B * G, 256)), dim3(256), 0, s, part, B, G, split,
+                     (double)HW * (C / G), eps, mean_rstd);
+  return rdmi::check_launch("groupnorm_finalize");
+}
+
+extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G, const float* mean_rstd,
+                                    const float* gamma, const float* beta, int silu, void* stream) {
+  RDMI_REQUIRE(x && y && mean_rstd && gamma && beta, RDMI_E_ARG, "groupnorm_apply: null pointer");
+  RDMI_REQUIRE(C % 8 == 0 && C % G == 0, RDMI_E_ARG, "groupnorm_apply: bad C=%d G=%d", C, G);
+  long nvec = (long)B * HW * C / 8;
+  long grid = (nvec + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(gn_apply, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, HW,
+                     C, G, nvec, mean_rstd, gamma, beta, silu);
+  return rdmi::check_launch("groupnorm_apply");
+}
+
+extern "C" int rdmi_layernorm(const void* x, void* y, long M, int C, const float* gamma, const float* beta, float eps,
+                              void* stream) {
+  RDMI_REQUIRE(x && y && gamma && beta, RDMI_E_ARG, "layernorm: null pointer");
+  RDMI_REQUIRE(C % 8 == 0 && C <= 2048 && M > 0, RDMI_E_ARG, "layernorm: bad C=%d", C);
+  hipLaunchKernelGGL(layernorm_k, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, (const f16*)x,
+                     (f16*)y, M, C, gamma, beta, eps);
+  return rdmi::check_launch("layernorm");
+}

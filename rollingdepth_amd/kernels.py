@@ -1,0 +1,376 @@
+"""Torch-tensor front end of librdmi: argument validation, output allocation (PyTorch caching
+allocator owns every buffer) and the current HIP stream.  No arithmetic happens here."""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native as _N
+from ._native import check, lib
+
+F16 = torch.float16
+F32 = torch.float32
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _need(t: torch.Tensor, dtype, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor, got {t.device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+# ----------------------------------------------------------------------------- weight packing
+def pack_linear(w: torch.Tensor, device) -> torch.Tensor:
+    """[N, K] → f16 [N, Kp] (K zero-padded to a multiple of 32)."""
+    n, k = w.shape
+    kp = (k + 31) // 32 * 32
+    out = torch.zeros((n, kp), dtype=F16, device=device)
+    out[:, :k] = w.to(device=device, dtype=F16)
+    return out
+
+
+def geglu_permute(w: torch.Tensor, b: torch.Tensor):
+    """Row permutation that puts value/gate rows of GEGLU's proj (out 2·I) side by side in
+    64-row slabs: slab s = [h rows 32s..32s+31, g rows 32s..32s+31] (gemm.hip GEGLU epilogue)."""
+    two_i = w.shape[0]
+    i = two_i // 2
+    assert i % 32 == 0
+    idx = []
+    for s in range(i // 32):
+        idx.extend(range(32 * s, 32 * s + 32))
+        idx.extend(range(i + 32 * s, i + 32 * s + 32))
+    idx = torch.tensor(idx, dtype=torch.long)
+    return w[idx], b[idx]
+
+
+def pad_channels(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> torch.Tensor:
+    """[Cout, Cin, kh, kw] → f16 [Cout, Kp] laid out [Cout][kh][kw][Cin_pad] (implicit-GEMM K
+    order of gemm.hip), zero padded to Kp % 32 == 0."""
+    co, ci, kh, kw = w.shape
+    cp = cin_pad or pad_channels(ci)
+    t = torch.zeros((co, kh, kw, cp), dtype=F32)
+    t[..., :ci] = w.permute(0, 2, 3, 1).float()
+    k = kh * kw * cp
+    kp = (k + 31) // 32 * 32
+    out = torch.zeros((co, kp), dtype=F16)
+    out[:, :k] = t.reshape(co, k).half()
+    return out.to(device)
+
+
+# ----------------------------------------------------------------------------- GEMM / conv
+def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
+         bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+         rowbias: Optional[torch.Tensor] = None, rows_per_group: int = 0, alpha: float = 1.0,
+         geglu: bool = False, out_f32: bool = False, n: Optional[int] = None) -> torch.Tensor:
+    """out[m, :] = alpha·a[m, :k] @ w[:, :k]ᵀ + bias (+ rowbias[m // rows_per_group]) (+ residual).
+    a: f16 [..., M, lda]; w: f16 [N, Kp]; batched over a leading dim when a is 3-D."""
+    _need(a, F16, "gemm.a")
+    _need(w, F16, "gemm.w")
+    batch = a.shape[0] if a.dim() == 3 else 1
+    M = a.shape[-2]
+    N = w.shape[0] if n is None else n
+    NO = N // 2 if geglu else N
+    if out is None:
+        shape = (batch, M, NO) if a.dim() == 3 else (M, NO)
+        out = torch.empty(shape, dtype=F32 if out_f32 else F16, device=a.device)
+    g = _gemm_args(a, w, out, bias, residual, rowbias, rows_per_group, alpha, M, N, k, batch, geglu, out_f32)
+    check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
+    return out
+
+
+def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, geglu, out_f32):
+    g = _N.GemmArgs()
+    g.A = a.data_ptr(); g.lda = a.stride(-2); g.strideA = a.stride(0) if a.dim() == 3 else 0
+    g.W = w.data_ptr(); g.ldw = w.stride(0); g.strideW = w.stride(0) * w.shape[0] if w.dim() == 3 else 0
+    if w.dim() == 3:
+        g.strideW = w.stride(0)
+        g.ldw = w.stride(1)
+    g.C = out.data_ptr(); g.ldc = out.stride(-2); g.strideC = out.stride(0) if out.dim() == 3 else 0
+    g.c_f32 = 1 if out_f32 else 0
+    g.bias = _p(bias)
+    g.residual = _p(residual)
+    if residual is not None:
+        g.ldr = residual.stride(-2)
+        g.strideR = residual.stride(0) if residual.dim() == 3 else 0
+    g.rowbias = _p(rowbias)
+    g.rows_per_group = rpg
+    g.rowbias_ld = rowbias.stride(0) if rowbias is not None else 0
+    g.alpha = alpha
+    g.M, g.N, g.K, g.batch = M, Nn, K, batch
+    g.epilogue = 1 if geglu else 0
+    return g
+
+
+def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1, pad: int = 1,
+           pad_tl: Optional[int] = None, upsample: bool = False, bias: Optional[torch.Tensor] = None,
+           residual: Optional[torch.Tensor] = None, rowbias: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, alpha: float = 1.0, out_hw=None) -> torch.Tensor:
+    """NHWC f16 conv.  x [B, H, W, Cin_pad]; w packed by pack_conv.  `pad` is symmetric; pad_tl
+    overrides the top/left padding with bottom/right implied by out_hw (VAE Downsample2D)."""
+    _need(x, F16, "conv2d.x")
+    _need(w, F16, "conv2d.w")
+    B, H, W, Cin = x.shape
+    Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
+    pt = pad if pad_tl is None else pad_tl
+    if out_hw is None:
+        Ho = (Hi + 2 * pad - k) // stride + 1
+        Wo = (Wi + 2 * pad - k) // stride + 1
+    else:
+        Ho, Wo = out_hw
+    if out is None:
+        out = torch.empty((B, Ho, Wo, cout), dtype=F16, device=x.device)
+    a = _N.ConvArgs()
+    a.x, a.w, a.y = x.data_ptr(), w.data_ptr(), out.data_ptr()
+    a.bias, a.residual, a.rowbias = _p(bias), _p(residual), _p(rowbias)
+    a.B, a.H, a.W, a.Cin, a.Cout, a.kh, a.kw = B, H, W, Cin, cout, k, k
+    a.stride, a.pad_top, a.pad_left, a.upsample, a.Ho, a.Wo = stride, pt, pt, int(upsample), Ho, Wo
+    a.Kp = w.shape[1]
+    a.y_ld = out.stride(-2)
+    a.res_ld = residual.stride(-2) if residual is not None else 0
+    a.alpha = alpha
+    if w.shape[1] < k * k * Cin:
+        raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
+    check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
+    return out
+
+
+# ----------------------------------------------------------------------------- norms
+_ws_cache = {}
+
+
+def _workspace(n_floats: int, device) -> torch.Tensor:
+    key = (device, "ws")
+    t = _ws_cache.get(key)
+    if t is None or t.numel() < n_floats:
+        t = torch.empty(max(n_floats, 1 << 16), dtype=F32, device=device)
+        _ws_cache[key] = t
+    return t
+
+
+def groupnorm_stats(x: torch.Tensor, groups: int, eps: float) -> torch.Tensor:
+    _need(x, F16, "groupnorm.x")
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (B * C)
+    mr = torch.empty((B * groups * 2,), dtype=F32, device=x.device)
+    ws = _workspace(lib.rdmi_groupnorm_workspace(B, groups), x.device)
+    check(lib.rdmi_groupnorm_stats(x.data_ptr(), B, HW, C, groups, eps, mr.data_ptr(), ws.data_ptr(), _stream()),
+          "rdmi_groupnorm_stats")
+    return mr
+
+
+def groupnorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float,
+              silu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    mr = groupnorm_stats(x, groups, eps)
+    B, C = x.shape[0], x.shape[-1]
+    HW = x.numel() // (B * C)
+    out = torch.empty_like(x) if out is None else out
+    check(lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), B, HW, C, groups, mr.data_ptr(), gamma.data_ptr(),
+                                   beta.data_ptr(), int(silu), _stream()), "rdmi_groupnorm_apply")
+    return out
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _need(x, F16, "layernorm.x")
+    C_ = x.shape[-1]
+    M = x.numel() // C_
+    out = torch.empty_like(x) if out is None else out
+    check(lib.rdmi_layernorm(x.data_ptr(), out.data_ptr(), M, C_, gamma.data_ptr(), beta.data_ptr(), eps, _stream()),
+          "rdmi_layernorm")
+    return out
+
+
+# ----------------------------------------------------------------------------- attention
+def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out: Optional[torch.Tensor] = None,
+              scale: Optional[float] = None) -> torch.Tensor:
+    """q/k/v: f16 [B, S, H*64] views (any row stride, unit column stride) → out [B, Sq, H*64]."""
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        _need(t, F16, f"attention.{nm}")
+        if t.stride(-1) != 1:
+            raise ValueError("attention: inner dim must be contiguous")
+    B, Sq, HD = q.shape
+    D = HD // heads
+    Sk = k.shape[1]
+    if out is None:
+        out = torch.empty((B, Sq, HD), dtype=F16, device=q.device)
+    sc = 1.0 / math.sqrt(D) if scale is None else scale
+    check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
+                                 q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
+                                 v.stride(0), out.stride(0), sc, _stream()), "rdmi_attention_fwd")
+    return out
+
+
+def attention_smallkv(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q [B, Sq, H*64] (row stride any), k/v [Bkv, L, H*64] contiguous with Bkv ∈ {1, B}."""
+    _need(q, F16, "attention_smallkv.q")
+    B, Sq, HD = q.shape
+    D = HD // heads
+    L = k.shape[1]
+    k = k.contiguous()
+    v = v.contiguous()
+    if out is None:
+        out = torch.empty((B, Sq, HD), dtype=F16, device=q.device)
+    kv_bs = 0 if k.shape[0] == 1 else k.stride(0)
+    check(lib.rdmi_attention_smallkv(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, L, D,
+                                     q.stride(1), out.stride(1), q.stride(0), out.stride(0), kv_bs,
+                                     1.0 / math.sqrt(D), _stream()), "rdmi_attention_smallkv")
+    return out
+
+
+def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _need(s, F32, "softmax_rows.s")
+    cols = s.shape[-1]
+    rows = s.numel() // cols
+    out = torch.empty(s.shape, dtype=F16, device=s.device) if out is None else out
+    check(lib.rdmi_softmax_rows(s.data_ptr(), out.data_ptr(), rows, cols, scale, _stream()), "rdmi_softmax_rows")
+    return out
+
+
+def transpose(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[B, R, Cc] (row stride any) → [B, Cc, R] contiguous."""
+    _need(src, F16, "transpose.src")
+    B, R, Cc = src.shape
+    out = torch.empty((B, Cc, R), dtype=F16, device=src.device) if out is None else out
+    check(lib.rdmi_transpose(src.data_ptr(), out.data_ptr(), B, R, Cc, src.stride(1), out.stride(1), _stream()),
+          "rdmi_transpose")
+    return out
+
+
+# ----------------------------------------------------------------------------- layout / misc
+def nchw_to_nhwc(x: torch.Tensor, cpad: int, scale: float = 1.0) -> torch.Tensor:
+    if not x.is_cuda or x.dtype not in (F16, F32):
+        raise TypeError("nchw_to_nhwc: device f16/f32 tensor expected")
+    x = x.contiguous()
+    B, Cc, H, W = x.shape
+    out = torch.empty((B, H, W, cpad), dtype=F16, device=x.device)
+    check(lib.rdmi_nchw_to_nhwc(x.data_ptr(), int(x.dtype == F32), out.data_ptr(), B, Cc, H, W, cpad, scale,
+                                _stream()), "rdmi_nchw_to_nhwc")
+    return out
+
+
+def nhwc_to_nchw_f32(x: torch.Tensor, c: int, scale: float = 1.0, shift: float = 0.0) -> torch.Tensor:
+    _need(x, F16, "nhwc_to_nchw.x")
+    B, H, W, Cl = x.shape
+    out = torch.empty((B, c, H, W), dtype=F32, device=x.device)
+    check(lib.rdmi_nhwc_to_nchw_f32(x.data_ptr(), x.stride(2), out.data_ptr(), B, c, H, W, scale, shift, _stream()),
+          "rdmi_nhwc_to_nchw_f32")
+    return out
+
+
+def concat_channels(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _need(a, F16, "concat.a")
+    _need(b, F16, "concat.b")
+    Ca, Cb = a.shape[-1], b.shape[-1]
+    P = a.numel() // Ca
+    out = torch.empty((*a.shape[:-1], Ca + Cb), dtype=F16, device=a.device) if out is None else out
+    check(lib.rdmi_concat_channels(a.data_ptr(), Ca, b.data_ptr(), Cb, out.data_ptr(), P, _stream()), "rdmi_concat")
+    return out
+
+
+def gather_unet_input(rgb: torch.Tensor, depth: torch.Tensor, frame_idx: torch.Tensor, depth_bcast: bool,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """rgb [N, h, w, 8] (channels 0..3 used), depth [N or 1, h, w, 8]; frame_idx int32 device."""
+    _need(rgb, F16, "gather.rgb")
+    cnt = frame_idx.numel()
+    _, h, w, _c = rgb.shape
+    out = torch.empty((cnt, h, w, 8), dtype=F16, device=rgb.device) if out is None else out
+    check(lib.rdmi_gather_unet_input(rgb.data_ptr(), rgb.stride(0), depth.data_ptr(), depth.stride(0),
+                                     int(depth_bcast), frame_idx.data_ptr(), cnt, h * w, out.data_ptr(), _stream()),
+          "rdmi_gather_unet_input")
+    return out
+
+
+def ddim_combine(x: torch.Tensor, e: torch.Tensor, ca: float, cb: float, out_scale: float, c: int, cpad: int,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """y[..., :c] = (ca·x + cb·e)·out_scale, y[..., c:cpad] = 0; x/e [P, ld] channel-last views."""
+    P = x.numel() // x.shape[-1]
+    out = torch.empty((*x.shape[:-1], cpad), dtype=F16, device=x.device) if out is None else out
+    check(lib.rdmi_ddim_combine(x.data_ptr(), x.stride(-2) if x.dim() >= 2 else x.shape[-1], e.data_ptr(),
+                                e.stride(-2) if e.dim() >= 2 else e.shape[-1], out.data_ptr(), out.stride(-2), P, c, cpad,
+                                ca, cb, out_scale, _stream()), "rdmi_ddim_combine")
+    return out
+
+
+def minmax(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype not in (F16, F32):
+        raise TypeError("minmax: f16/f32 expected")
+    out = torch.empty(2, dtype=F32, device=x.device)
+    ws = _workspace(2048, x.device)
+    check(lib.rdmi_minmax(x.data_ptr(), int(x.dtype == F32), x.numel(), out.data_ptr(), ws.data_ptr(), _stream()),
+          "rdmi_minmax")
+    return out
+
+
+def renormalize_(x: torch.Tensor, mm: torch.Tensor) -> torch.Tensor:
+    _need(x, F32, "renormalize.x")
+    check(lib.rdmi_renormalize_f32(x.data_ptr(), x.numel(), mm.data_ptr(), _stream()), "rdmi_renormalize")
+    return x
+
+
+# ----------------------------------------------------------------------------- aligner
+def aligner_prepare(x: torch.Tensor, shift: torch.Tensor, border: int, factor: int) -> torch.Tensor:
+    """x [n, w, H, W] f16/f32 → f32 [n, w, P]."""
+    n, w, H, W = x.shape
+    hs = (H - 2 * border + factor - 1) // factor
+    ws_ = (W - 2 * border + factor - 1) // factor
+    out = torch.empty((n, w, hs * ws_), dtype=F32, device=x.device)
+    check(lib.rdmi_aligner_prepare(x.data_ptr(), int(x.dtype == F32), n, w, H, W, border, factor, shift.data_ptr(),
+                                   out.data_ptr(), _stream()), "rdmi_aligner_prepare")
+    return out
+
+
+def aligner_optimize(xs: Sequence[torch.Tensor], scales: Sequence[torch.Tensor], trans: Sequence[torch.Tensor],
+                     strides: Sequence[int], seq_len: int, lr: float, betas, eps: float, lmda2: float, lmda3: float,
+                     depth_w: float, loss_scale: float, iters: int, history: Optional[torch.Tensor]):
+    a = _N.AlignerArgs()
+    a.n_dil = len(xs)
+    for d, (x, s, t, st) in enumerate(zip(xs, scales, trans, strides)):
+        _need(x, F32, "aligner.x")
+        a.x[d] = x.data_ptr()
+        a.s[d] = s.data_ptr()
+        a.t[d] = t.data_ptr()
+        a.n[d] = x.shape[0]
+        a.stride[d] = st
+    a.w = xs[0].shape[1]
+    a.seq_len = seq_len
+    a.P = xs[0].shape[2]
+    a.lr, a.beta1, a.beta2, a.eps = lr, betas[0], betas[1], eps
+    a.lmda2, a.lmda3, a.depth_w, a.loss_scale = lmda2, lmda3, depth_w, loss_scale
+    a.iters = iters
+    a.history = _p(history)
+    nws = lib.rdmi_aligner_workspace(C.byref(a))
+    ws = torch.empty(nws + 16, dtype=F32, device=xs[0].device)
+    a.workspace = ws.data_ptr()
+    check(lib.rdmi_aligner_optimize(C.byref(a), _stream()), "rdmi_aligner_optimize")
+    return ws  # keep alive until the stream has consumed it
+
+
+def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: int, shift: torch.Tensor) -> torch.Tensor:
+    """xf[d] [n_d, w, H, W] (f16/f32) → [seq_len, H, W] f32."""
+    nd = len(xf)
+    n_, w, H, W = xf[0].shape
+    out = torch.empty((seq_len, H, W), dtype=F32, device=xf[0].device)
+    xp = (C.c_void_p * nd)(*[x.data_ptr() for x in xf])
+    sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
+    tp = (C.c_void_p * nd)(*[t.data_ptr() for t in trans])
+    nn = (C.c_int * nd)(*[x.shape[0] for x in xf])
+    stv = (C.c_int * nd)(*list(strides))
+    check(lib.rdmi_aligner_merge(nd, xp, int(xf[0].dtype == F32), sp, tp, nn, stv, w, seq_len, H * W,
+                                 shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge")
+    return out

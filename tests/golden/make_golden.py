@@ -1,0 +1,262 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Build-container only (needs /root/reference, read-only; see _refload.py).  The GPU box never
+runs this; it only reads the committed .safetensors / .json outputs.
+
+    python tests/golden/make_golden.py [--skip-sd2]
+
+Fixtures (all inputs synthesised deterministically, rollingdepth_amd/weights.py):
+  keys_sd2_unet.json / keys_sd2_vae.json    state-dict key→shape of the reference modules
+  tiny_pipeline.safetensors (+ .json)       RollingDepthPipeline.forward, tiny UNet/VAE, 9 frames
+                                            32², dilations [1,3] (capped by the reference), fp32
+  sd2_256.safetensors (+ .json)             config 1: 3 frames 256², SD2-shaped, dil [1], fp32,
+                                            cap_dilation=False, aligner 2000 it
+  attn_processor.safetensors                modified AttnProcessor2_0 (num_view=3 self / cross,
+                                            VAE-style 4-D group_norm+residual), fp32
+  aligner.safetensors (+ .json)             DepthAligner.run on synthetic snippets, dil [1,4]
+  ddim.json                                 DDIMScheduler timesteps / step / add_noise values
+  snippet_indices.json                      get_snippet_indice / cap_max_dilation / aligner indices
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from safetensors.torch import save_file  # noqa: E402
+
+import _refload  # noqa: E402
+from rollingdepth_amd import config as C  # noqa: E402
+from rollingdepth_amd import weights as W  # noqa: E402
+
+
+def _c(t):
+    return t.detach().to(torch.float32).contiguous().clone()
+
+
+def build_pipe(P, ucfg, vcfg, scfg, seed=0):
+    from diffusers import AutoencoderKL, DDIMScheduler, UNet2DConditionModel
+
+    unet = UNet2DConditionModel(**ucfg)
+    vae = AutoencoderKL(**vcfg)
+    unet.load_state_dict(W.synth_state_dict(W.unet_param_shapes(ucfg), seed), strict=True)
+    vae.load_state_dict(W.synth_state_dict(W.vae_param_shapes(vcfg), seed), strict=True)
+    sched = DDIMScheduler(**scfg)
+    pipe = P.RollingDepthPipeline(unet=unet, vae=vae, scheduler=sched, text_encoder=None, tokenizer=None)
+    pipe.empty_text_embed = W.synth_context(ucfg["cross_attention_dim"], seed)
+    return pipe
+
+
+def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None):
+    rec = {"unet_out": [], "snip_lat": []}
+    orig_single = pipe.single_step
+    orig_dec = pipe.decode_depth
+    orig_enc = pipe.encode_rgb
+
+    def single(**kw):
+        out = orig_single(**kw)
+        rec["unet_out"].append(_c(out[0]))
+        return out
+
+    def enc(x, **kw):
+        out = orig_enc(x, **kw)
+        rec.setdefault("rgb_latent", _c(out[0]))
+        return out
+
+    def dec(lat, **kw):
+        rec["snip_lat"].append(_c(lat))
+        return orig_dec(lat, **kw)
+
+    pipe.single_step = single
+    pipe.decode_depth = dec
+    pipe.encode_rgb = enc
+    dil = list(dilations)
+    g = torch.Generator().manual_seed(noise_seed)
+    with torch.no_grad():
+        out = pipe.forward(
+            input_frames=frames[None], dilations=dil, cap_dilation=cap, snippet_lengths=[3],
+            init_infer_steps=[1], strides=[1], coalign_kwargs=coalign, refine_step=0,
+            refine_snippet_len=3, refine_start_dilation=6, generator=g, verbose=False,
+            max_vae_bs=4, unload_snippet=False)
+    rec["dilations_used"] = dil  # forward mutates the caller's list in place (:246-252)
+    return out, rec
+
+
+def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None):
+    pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
+    h, w = frames.shape[-2] // C.vae_downscale(vcfg), frames.shape[-1] // C.vae_downscale(vcfg)
+    noise = torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(1))
+    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign)
+    t = {
+        "frames": _c(frames), "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
+        "rgb_latent": rec["rgb_latent"], "depth_pred": _c(out.depth_pred),
+        "depth_coaligned": _c(out.depth_coaligned),
+        "unet_out_first": rec["unet_out"][0], "unet_out_last": rec["unet_out"][-1],
+    }
+    for i, (lat, sn) in enumerate(zip(rec["snip_lat"], out.snippet_ls)):
+        t[f"snippet_latent_{i}"] = lat
+        t[f"snippet_{i}"] = _c(sn)
+    save_file(t, os.path.join(HERE, name + ".safetensors"))
+    meta = {"dilations_in": list(dilations), "dilations_used": rec["dilations_used"], "cap_dilation": cap,
+            "unet": ucfg, "vae": vcfg, "scheduler": C.RD_SCHEDULER, "coalign": coalign or {}}
+    json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
+    print(name, {k: tuple(v.shape) for k, v in t.items()})
+
+
+def attn_fixture():
+    from diffusers.models.attention_processor import Attention, AttnProcessor2_0
+
+    torch.manual_seed(0)
+    out = {}
+    # UNet self-attention (attn1) with the num_view fold; L0-like width, reduced hw.
+    a = Attention(query_dim=320, heads=5, dim_head=64, bias=False, out_bias=True)
+    a.set_processor(AttnProcessor2_0())
+    sd = W.synth_state_dict({k: tuple(v.shape) for k, v in a.state_dict().items()}, 7)
+    a.load_state_dict(sd)
+    x = torch.randn(3, 64, 320)
+    with torch.no_grad():
+        y = a(x, num_view=3)
+        y1 = a(x)  # num_view=None: per-frame attention
+    out.update({"self_x": x, "self_y_nv3": _c(y), "self_y_nv_none": _c(y1)})
+    shapes = {"self": {k: list(t.shape) for k, t in sd.items()}}
+    # cross-attention (attn2) against a 2-token context, num_view folded.
+    c = Attention(query_dim=320, cross_attention_dim=1024, heads=5, dim_head=64, bias=False, out_bias=True)
+    c.set_processor(AttnProcessor2_0())
+    sdc = W.synth_state_dict({k: tuple(v.shape) for k, v in c.state_dict().items()}, 8)
+    c.load_state_dict(sdc)
+    ctx = torch.randn(1, 2, 1024)
+    with torch.no_grad():
+        yc = c(x, encoder_hidden_states=ctx, num_view=3)
+    out.update({"cross_ctx": ctx, "cross_y_nv3": _c(yc)})
+    shapes["cross"] = {k: list(t.shape) for k, t in sdc.items()}
+    # VAE mid-block attention: group_norm, 1 head d=C, biased, residual, 4-D input.
+    v = Attention(query_dim=128, heads=1, dim_head=128, rescale_output_factor=1.0, eps=1e-6,
+                  norm_num_groups=32, spatial_norm_dim=None, residual_connection=True, bias=True,
+                  upcast_softmax=True, _from_deprecated_attn_block=True)
+    v.set_processor(AttnProcessor2_0())
+    sdv = W.synth_state_dict({k: tuple(t.shape) for k, t in v.state_dict().items()}, 9)
+    v.load_state_dict(sdv)
+    xv = torch.randn(2, 128, 8, 8)
+    with torch.no_grad():
+        yv = v(xv)
+    out.update({"vae_x": xv, "vae_y": _c(yv)})
+    shapes["vae"] = {k: list(t.shape) for k, t in sdv.items()}
+    shapes["seeds"] = {"self": 7, "cross": 8, "vae": 9}
+    json.dump(shapes, open(os.path.join(HERE, "attn_processor.json"), "w"), indent=1)
+    save_file({k: t.contiguous() for k, t in out.items()}, os.path.join(HERE, "attn_processor.safetensors"))
+    print("attn_processor", len(out))
+
+
+def aligner_fixture(A):
+    g = torch.Generator().manual_seed(3)
+    N, H, Wd = 20, 64, 64
+    dil = [1, 4]
+    base = torch.rand((N, 1, H, Wd), generator=g) * 2 - 1
+    snips = []
+    for d in dil:
+        gap = d
+        n = N - 2 * gap
+        s = torch.stack([torch.stack([base[i + j * gap] for j in range(3)]) for i in range(n)])
+        sc = 0.5 + torch.rand((n, 1, 1, 1, 1), generator=g)
+        sh = 0.3 * torch.randn((n, 1, 1, 1, 1), generator=g)
+        snips.append((s * sc + sh + 0.01 * torch.randn(s.shape, generator=g)).float())
+    al = A.DepthAligner(device=torch.device("cpu"), num_iterations=2000)
+    merged, s, t, hist = al.run([x.clone() for x in snips], list(dil))
+    out = {f"snippet_{i}": x for i, x in enumerate(snips)}
+    out.update({"merged": _c(merged)})
+    for i, (a, b) in enumerate(zip(s, t)):
+        out[f"scale_{i}"] = _c(a)
+        out[f"trans_{i}"] = _c(b)
+    out["loss_hist"] = torch.tensor(np.array(hist, dtype=np.float64))
+    save_file(out, os.path.join(HERE, "aligner.safetensors"))
+    json.dump({"dilations": dil, "N": N, "H": H, "W": Wd, "iterations": 2000},
+              open(os.path.join(HERE, "aligner.json"), "w"))
+    print("aligner", merged.shape)
+
+
+def ddim_fixture():
+    from diffusers import DDIMScheduler
+
+    s = DDIMScheduler(**C.RD_SCHEDULER)
+    res = {"alphas_cumprod_0": float(s.alphas_cumprod[0]), "alphas_cumprod_999": float(s.alphas_cumprod[999]),
+           "final_alpha_cumprod": float(s.final_alpha_cumprod)}
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 4, 3, 3, generator=g)
+    o = torch.randn(2, 4, 3, 3, generator=g)
+    for n in (1, 4, 10, 20):
+        s.set_timesteps(n)
+        ts = [int(t) for t in s.timesteps]
+        res[f"timesteps_{n}"] = ts
+        res[f"step_{n}_t0"] = s.step(o, ts[0], x).prev_sample.flatten().tolist()
+        res[f"step_{n}_tlast"] = s.step(o, ts[-1], x).prev_sample.flatten().tolist()
+    res["add_noise_499"] = s.add_noise(x, o, torch.tensor([499])).flatten().tolist()
+    res["x"] = x.flatten().tolist()
+    res["o"] = o.flatten().tolist()
+    json.dump(res, open(os.path.join(HERE, "ddim.json"), "w"))
+    print("ddim", list(res)[:6])
+
+
+def index_fixture(P, A):
+    RDP = P.RollingDepthPipeline
+    res = {"cap": [], "snippets": [], "aligner": []}
+    for n in (3, 6, 9, 10, 25, 100, 500):
+        for d in (1, 3, 10, 25):
+            res["cap"].append([n, 3, d, RDP.cap_max_dilation(n, 3, d, False)])
+    for n, d in ((9, 1), (9, 2), (100, 1), (100, 25), (500, 10), (500, 25), (12, 5)):
+        ts = torch.tensor([999])
+        res["snippets"].append([n, d, RDP.get_snippet_indice(0, ts, n, 3, d, d, 1)])
+    for i_step, T in ((0, 5), (2, 5), (4, 5)):
+        ts = torch.arange(T)
+        res["snippets"].append([50, [6, 1, i_step, T], RDP.get_snippet_indice(i_step, ts, 50, 3, 6, 1, 1)])
+    al = A.DepthAligner(device=torch.device("cpu"))
+    for n, gap in ((9, 0), (9, 1), (100, 24), (500, 9)):
+        res["aligner"].append([n, gap, al.create_triplet_indices(n, gap, 3).tolist()])
+    json.dump(res, open(os.path.join(HERE, "snippet_indices.json"), "w"))
+    print("indices ok")
+
+
+def keys_fixture():
+    from diffusers import AutoencoderKL, UNet2DConditionModel
+
+    with torch.device("meta"):
+        u = UNet2DConditionModel(**C.SD2_UNET)
+        v = AutoencoderKL(**C.SD2_VAE)
+    json.dump({k: list(t.shape) for k, t in u.state_dict().items()}, open(os.path.join(HERE, "keys_sd2_unet.json"), "w"))
+    json.dump({k: list(t.shape) for k, t in v.state_dict().items()}, open(os.path.join(HERE, "keys_sd2_vae.json"), "w"))
+    print("keys ok")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-sd2", action="store_true")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    torch.set_num_threads(os.cpu_count() or 8)
+    P, A = _refload.load_reference()
+    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "sd2"]
+    if "keys" in todo:
+        keys_fixture()
+    if "idx" in todo:
+        index_fixture(P, A)
+    if "ddim" in todo:
+        ddim_fixture()
+    if "attn" in todo:
+        attn_fixture()
+    if "aligner" in todo:
+        aligner_fixture(A)
+    if "tiny" in todo:
+        frames = W.synth_frames(9, 32, 32, seed=0)
+        pipeline_fixture(P, "tiny_pipeline", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True)
+    if "sd2" in todo and not a.skip_sd2:
+        frames = W.synth_frames(3, 256, 256, seed=0)
+        pipeline_fixture(P, "sd2_256", C.SD2_UNET, C.SD2_VAE, frames, [1], False)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,58 @@
+"""DepthAligner kernels (aligner.hip) vs the numpy oracle (oracle/rd_oracle.py), which is itself
+pinned to the reference's DepthAligner.run in tests/test_oracle_golden.py."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import rd_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _synth(N=14, dil=(1, 3), H=40, W=44, seed=0, dtype=np.float32):
+    rng = np.random.default_rng(seed)
+    base = rng.uniform(-1, 1, (N, 1, H, W)).astype(np.float32)
+    out = []
+    for d in dil:
+        n = N - 2 * d
+        s = np.stack([np.stack([base[i + j * d] for j in range(3)]) for i in range(n)])
+        sc = 0.5 + rng.uniform(0, 1, (n, 1, 1, 1, 1))
+        sh = 0.3 * rng.standard_normal((n, 1, 1, 1, 1))
+        out.append((s * sc + sh + 0.01 * rng.standard_normal(s.shape)).astype(dtype))
+    return out, list(dil)
+
+
+@pytest.mark.parametrize("iters", [1, 50, 400])
+def test_aligner_optimize_matches_oracle(iters):
+    from rollingdepth_amd.aligner import DepthAligner
+
+    snips, dil = _synth()
+    ref_m, ref_s, ref_t, ref_h = O.aligner_run(snips, dil, iters=iters)
+    al = DepthAligner(device=torch.device(DEV), num_iterations=iters)
+    m, s, t, h = al.run([torch.from_numpy(x).to(DEV) for x in snips], list(dil))
+    for d in range(len(dil)):
+        assert np.abs(s[d].cpu().numpy().ravel() - ref_s[d]).max() < 2e-5 * max(1, iters / 50)
+        assert np.abs(t[d].cpu().numpy().ravel() - ref_t[d]).max() < 2e-5 * max(1, iters / 50)
+    assert abs(h[0][0] - ref_h[0][0]) < 1e-5 * abs(ref_h[0][0]) + 1e-7
+    assert np.abs(m.cpu().numpy() - ref_m).max() < 1e-4
+
+
+def test_aligner_merge_f16_rounding():
+    from rollingdepth_amd import kernels as K
+
+    snips, dil = _synth(seed=1, dtype=np.float16)
+    rng = np.random.default_rng(2)
+    sc = [(1 + 0.1 * rng.standard_normal(x.shape[0])).astype(np.float32) for x in snips]
+    tr = [(0.1 * rng.standard_normal(x.shape[0])).astype(np.float32) for x in snips]
+    mn = min(float(x.min()) for x in snips)
+    shifted = [(x - np.float16(mn)).astype(np.float16) for x in snips]
+    N = 14
+    idx = [O.aligner_indices(N, d - 1, 3) for d in dil]
+    ref = O.aligner_merge(shifted, idx, sc, tr, N)
+    xf = [torch.from_numpy(x[:, :, 0]).to(DEV) for x in snips]
+    shift = torch.tensor([mn], dtype=torch.float32, device=DEV)
+    out = K.aligner_merge(xf, [torch.from_numpy(s).to(DEV) for s in sc], [torch.from_numpy(t).to(DEV) for t in tr],
+                          dil, N, shift)
+    got = out.half().float().cpu().numpy()
+    assert np.abs(got - ref[:, 0].astype(np.float32)).max() <= 2e-3

@@ -1,0 +1,235 @@
+"""Op-level numerics of librdmi on the MI355X, each against a plain PyTorch fp32 reference of the
+same op computed from the same f16-rounded inputs (tolerances stated per test: f16 storage of the
+output dominates, ~2⁻¹¹ relative)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _k():
+    from rollingdepth_amd import kernels as K
+    return K
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 320, 320), (1000, 960, 320), (77, 64, 1024), (5, 1280, 320),
+                                   (513, 200, 40)])
+def test_gemm_bias_residual(M, N, K):
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(0)
+    a = torch.randn(M, K, device=DEV, generator=g).half()
+    w = torch.randn(N, K, device=DEV, generator=g).half() / math.sqrt(K)
+    b = torch.randn(N, device=DEV, generator=g)
+    r = torch.randn(M, N, device=DEV, generator=g).half()
+    wp = K_.pack_linear(w.float(), DEV)
+    y = K_.gemm(a, wp, K, bias=b, residual=r)
+    ref = a.float() @ w.float().t() + b + r.float()
+    assert _rel(y, ref) < 4e-3
+
+
+def test_gemm_rowbias_alpha_f32out_batched():
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    B, M, N, K = 3, 200, 256, 96
+    a = torch.randn(B, M, K, device=DEV, generator=g).half()
+    w = torch.randn(B, N, K, device=DEV, generator=g).half()
+    y = K_.gemm(a, w, K, alpha=0.125, out_f32=True)
+    ref = torch.bmm(a.float(), w.float().transpose(1, 2)) * 0.125
+    assert _rel(y, ref) < 1e-5 * 50
+    rb = torch.randn(4, N, device=DEV, generator=g)
+    a2 = torch.randn(400, K, device=DEV, generator=g).half()
+    w2 = K_.pack_linear(torch.randn(N, K, device=DEV, generator=g), DEV)
+    y2 = K_.gemm(a2, w2, K, rowbias=rb, rows_per_group=100)
+    ref2 = a2.float() @ w2[:, :K].float().t() + rb.repeat_interleave(100, 0)
+    assert _rel(y2, ref2) < 4e-3
+
+
+def test_gemm_geglu():
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(2)
+    M, C = 333, 320
+    a = torch.randn(M, C, device=DEV, generator=g).half()
+    w = torch.randn(8 * C, C, device=DEV, generator=g) / math.sqrt(C)
+    b = torch.randn(8 * C, device=DEV, generator=g) * 0.1
+    wp, bp = K_.geglu_permute(w.cpu(), b.cpu())
+    y = K_.gemm(a, K_.pack_linear(wp, DEV), C, bias=bp.to(DEV), geglu=True)
+    h, gate = (a.float() @ w.half().float().t() + b).chunk(2, dim=-1)
+    ref = h * F.gelu(gate)
+    assert y.shape == (M, 4 * C)
+    assert _rel(y, ref) < 4e-3
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,pad,up", [
+    (2, 16, 16, 320, 320, 3, 1, 1, False), (1, 24, 20, 8, 320, 3, 1, 1, False), (2, 12, 12, 128, 128, 3, 2, 1, False),
+    (1, 9, 7, 64, 64, 3, 1, 1, True), (2, 10, 10, 3, 32, 3, 1, 1, False), (1, 8, 8, 64, 4, 3, 1, 1, False),
+    (2, 11, 13, 40, 24, 1, 1, 0, False)])
+def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up):
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(B, Cin, H, W, device=DEV, generator=g).half()
+    w = (torch.randn(Cout, Cin, k, k, device=DEV, generator=g) / math.sqrt(Cin * k * k)).half()
+    b = torch.randn(Cout, device=DEV, generator=g)
+    xin = F.interpolate(x.float(), scale_factor=2.0, mode="nearest") if up else x.float()
+    ref = F.conv2d(xin, w.float(), b, stride=stride, padding=pad)
+    cp = K_.pad_channels(Cin)
+    xn = K_.nchw_to_nhwc(x, cp)
+    y = K_.conv2d(xn, K_.pack_conv(w.float().cpu(), DEV, cp), Cout, k, stride=stride, pad=pad, upsample=up, bias=b)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
+
+
+def test_conv2d_vae_downsample_rowbias_residual():
+    """Downsample2D with padding=0: F.pad(0,1,0,1) then 3x3 s2 (downsampling.py:141-146)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(4)
+    B, C, H, W = 2, 64, 16, 16
+    x = torch.randn(B, C, H, W, device=DEV, generator=g).half()
+    w = (torch.randn(C, C, 3, 3, device=DEV, generator=g) / 24).half()
+    ref = F.conv2d(F.pad(x.float(), (0, 1, 0, 1)), w.float(), stride=2)
+    y = K_.conv2d(K_.nchw_to_nhwc(x, C), K_.pack_conv(w.float().cpu(), DEV), C, 3, stride=2, pad=0, pad_tl=0,
+                  out_hw=(H // 2, W // 2))
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
+    rb = torch.randn(B, C, device=DEV, generator=g)
+    res = torch.randn(B, H, W, C, device=DEV, generator=g).half()
+    y2 = K_.conv2d(K_.nchw_to_nhwc(x, C), K_.pack_conv(w.float().cpu(), DEV), C, 3, rowbias=rb, residual=res)
+    ref2 = F.conv2d(x.float(), w.float(), padding=1) + rb[:, :, None, None] + res.float().permute(0, 3, 1, 2)
+    assert _rel(y2.permute(0, 3, 1, 2), ref2) < 4e-3
+
+
+@pytest.mark.parametrize("C,G,HW,silu,eps", [(320, 32, 9216, True, 1e-5), (128, 32, 1000, False, 1e-6),
+                                            (2560, 32, 64, True, 1e-5), (1920, 32, 100, True, 1e-5),
+                                            (40, 8, 77, False, 1e-6)])
+def test_groupnorm(C, G, HW, silu, eps):
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B = 3
+    x = (torch.randn(B, HW, C, device=DEV, generator=g) * 2 + 0.7).half()
+    gm = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
+    bt = 0.1 * torch.randn(C, device=DEV, generator=g)
+    y = K_.groupnorm(x, gm, bt, G, eps, silu)
+    ref = F.group_norm(x.float().permute(0, 2, 1), G, gm, bt, eps).permute(0, 2, 1)
+    if silu:
+        ref = F.silu(ref)
+    assert (y.float() - ref).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("C", [320, 640, 1280])
+def test_layernorm(C):
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = (torch.randn(3, 577, C, device=DEV, generator=g) * 3).half()
+    gm = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
+    bt = 0.1 * torch.randn(C, device=DEV, generator=g)
+    y = K_.layernorm(x, gm, bt, 1e-5)
+    ref = F.layer_norm(x.float(), (C,), gm, bt, 1e-5)
+    assert (y.float() - ref).abs().max().item() < 1e-2
+
+
+def _sdpa_ref(q, k, v, heads):
+    B, Sq, HD = q.shape
+    D = HD // heads
+    qh = q.float().view(B, Sq, heads, D).transpose(1, 2)
+    kh = k.float().view(B, -1, heads, D).transpose(1, 2)
+    vh = v.float().view(B, -1, heads, D).transpose(1, 2)
+    o = F.scaled_dot_product_attention(qh, kh, vh)
+    return o.transpose(1, 2).reshape(B, Sq, HD)
+
+
+@pytest.mark.parametrize("B,S,H", [(1, 192, 2), (2, 768, 5), (1, 432, 20), (3, 100, 1), (1, 3072, 5), (2, 65, 3)])
+def test_attention_fused_qkv(B, S, H):
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(7)
+    C = H * 64
+    qkv = torch.randn(B, S, 3 * C, device=DEV, generator=g).half()
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    o = K_.attention(q, k, v, H)
+    ref = _sdpa_ref(q, k, v, H)
+    assert (o.float() - ref).abs().max().item() < 5e-3
+
+
+def test_attention_softmax_rescale_branch():
+    """A key spike late in the sequence forces the running-max rescale (guide rule 26)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(8)
+    B, S, H = 1, 640, 2
+    C = H * 64
+    q = torch.randn(B, S, C, device=DEV, generator=g).half()
+    k = torch.randn(B, S, C, device=DEV, generator=g).half()
+    v = torch.randn(B, S, C, device=DEV, generator=g).half()
+    k[0, 500] = (q[0, 3] * 3).half()  # query 3's max jumps at tile 7
+    o = K_.attention(q, k, v, H)
+    ref = _sdpa_ref(q, k, v, H)
+    assert (o.float() - ref).abs().max().item() < 5e-3
+
+
+def test_attention_smallkv():
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    B, S, H, L = 2, 999, 5, 2
+    C = H * 64
+    q = torch.randn(B, S, C, device=DEV, generator=g).half()
+    k = torch.randn(1, L, C, device=DEV, generator=g).half()
+    v = torch.randn(1, L, C, device=DEV, generator=g).half()
+    o = K_.attention_smallkv(q, k, v, H)
+    ref = _sdpa_ref(q, k.expand(B, -1, -1), v.expand(B, -1, -1), H)
+    assert (o.float() - ref).abs().max().item() < 3e-3
+
+
+def test_vae_style_attention_via_gemm():
+    """GEMM(f32 scores) → softmax_rows → GEMM with Vᵀ, the d=C single-head path."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(10)
+    B, S, D = 2, 256, 128
+    q = torch.randn(B, S, D, device=DEV, generator=g).half()
+    k = torch.randn(B, S, D, device=DEV, generator=g).half()
+    v = torch.randn(B, S, D, device=DEV, generator=g).half()
+    s = K_.gemm(q, k, D, out_f32=True)
+    p = K_.softmax_rows(s, 1.0 / math.sqrt(D))
+    vt = K_.transpose(v)
+    o = K_.gemm(p, vt, S)
+    ref = F.scaled_dot_product_attention(q.float()[:, None], k.float()[:, None], v.float()[:, None])[:, 0]
+    assert (o.float() - ref).abs().max().item() < 5e-3
+
+
+def test_layout_and_elementwise():
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(2, 3, 5, 7, device=DEV, generator=g)
+    n = K_.nchw_to_nhwc(x, 8, scale=2.0)
+    assert torch.allclose(n[..., :3].float(), (x * 2).permute(0, 2, 3, 1), atol=1e-2)
+    assert n[..., 3:].abs().max().item() == 0
+    back = K_.nhwc_to_nchw_f32(n, 3, scale=0.5, shift=1.0)
+    assert torch.allclose(back, x + 1.0, atol=1e-2)
+    a = torch.randn(10, 16, device=DEV, generator=g).half()
+    b = torch.randn(10, 24, device=DEV, generator=g).half()
+    assert torch.equal(K_.concat_channels(a, b), torch.cat([a, b], -1))
+    t = torch.randn(3, 70, 130, device=DEV, generator=g).half()
+    assert torch.equal(K_.transpose(t), t.transpose(1, 2).contiguous())
+    rgb = torch.randn(6, 4, 4, 8, device=DEV, generator=g).half()
+    dep = torch.randn(1, 4, 4, 8, device=DEV, generator=g).half()
+    idx = torch.tensor([0, 2, 4, 1, 3, 5], dtype=torch.int32, device=DEV)
+    u = K_.gather_unet_input(rgb, dep, idx, True)
+    assert torch.equal(u[..., :4], rgb[idx.long(), ..., :4])
+    assert torch.equal(u[..., 4:], dep[..., :4].expand(6, -1, -1, -1))
+    e = torch.randn(6, 4, 4, 4, device=DEV, generator=g).half()
+    y = K_.ddim_combine(u[..., 4:], e, 0.3, -0.7, 2.0, 4, 8)
+    ref = (0.3 * u[..., 4:].float() - 0.7 * e.float()) * 2.0
+    assert torch.allclose(y[..., :4].float(), ref, atol=1e-2) and y[..., 4:].abs().max().item() == 0
+    z = torch.randn(100003, device=DEV, generator=g)
+    mm = K_.minmax(z)
+    assert mm[0].item() == z.min().item() and mm[1].item() == z.max().item()
+    zr = z.clone()
+    K_.renormalize_(zr, mm)
+    ref = z - z.min()
+    ref = ref / ref.max()
+    ref = ref * 2.0 - 1.0
+    assert torch.equal(zr, ref)
