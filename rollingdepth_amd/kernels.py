@@ -83,7 +83,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     _need(w, F16, "gemm.w")
     batch = a.shape[0] if a.dim() == 3 else 1
     M = a.shape[-2]
-    N = w.shape[0] if n is None else n
+    N = w.shape[-2] if n is None else n
     NO = N // 2 if geglu else N
     if out is None:
         shape = (batch, M, NO) if a.dim() == 3 else (M, NO)

@@ -97,7 +97,7 @@ def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None):
         "frames": _c(frames), "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
         "rgb_latent": rec["rgb_latent"], "depth_pred": _c(out.depth_pred),
         "depth_coaligned": _c(out.depth_coaligned),
-        "unet_out_first": rec["unet_out"][0], "unet_out_last": rec["unet_out"][-1],
+        "unet_out_first": rec["unet_out"][0].clone(), "unet_out_last": rec["unet_out"][-1].clone(),
     }
     for i, (lat, sn) in enumerate(zip(rec["snip_lat"], out.snippet_ls)):
         t[f"snippet_latent_{i}"] = lat
