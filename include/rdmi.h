@@ -30,6 +30,7 @@ extern "C" {
 
 #define RDMI_EPI_NONE 0
 #define RDMI_EPI_GEGLU 1 /* out[:, n] = (h + b_h) * gelu_erf(g + b_g), weights row-interleaved */
+#define RDMI_EPI_SILU 2  /* out = silu(acc·alpha + bias ...) (TimestepEmbedding act, embeddings.py:543) */
 
 /* ---------------------------------------------------------------------------------------
  * Library
@@ -62,7 +63,7 @@ int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
 /* ---------------------------------------------------------------------------------------
  * Convolution as implicit GEMM on NHWC f16 (MFMA 16x16x32 f16, f32 accumulate).
  * y[b, ho, wo, co] = alpha * Σ w[co, dy, dx, ci] x[b, ho*s - pt + dy, wo*s - pl + dx, ci]
- *                    (+ bias[co]) (+ rowbias[b][co]) (+ residual[b, ho, wo, co])
+ *                    (+ bias[co]) (+ rowbias[b * rowbias_ld + co]) (+ residual[b, ho, wo, co])
  * `upsample`=1 reads x through a nearest ×2 upsample (Upsample2D, upsampling.py:141-190) without
  * materialising it.  Cin % 8 == 0 (pad channels); w is [Cout][kh][kw][Cin] padded to Kp % 32 == 0.
  * Replaces the cuDNN conv2d of ResnetBlock2D.conv1/conv2/conv_shortcut (resnet.py:320-373),
@@ -73,7 +74,7 @@ typedef struct rdmi_conv_args {
   const void* x; const void* w; void* y;
   const float* bias; const void* residual; const float* rowbias;
   int B, H, W, Cin, Cout, kh, kw, stride, pad_top, pad_left, upsample, Ho, Wo, Kp;
-  long y_ld; long res_ld; float alpha;
+  long y_ld; long res_ld; float alpha; long rowbias_ld; /* 0: one row shared by all images */
 } rdmi_conv_args;
 int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
 

@@ -38,7 +38,7 @@ class ConvArgs(C.Structure):
         ("B", i32), ("H", i32), ("W", i32), ("Cin", i32), ("Cout", i32), ("kh", i32), ("kw", i32),
         ("stride", i32), ("pad_top", i32), ("pad_left", i32), ("upsample", i32), ("Ho", i32), ("Wo", i32),
         ("Kp", i32),
-        ("y_ld", i64), ("res_ld", i64), ("alpha", f32),
+        ("y_ld", i64), ("res_ld", i64), ("alpha", f32), ("rowbias_ld", i64),
     ]
 
 

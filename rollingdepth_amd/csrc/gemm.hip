@@ -24,7 +24,7 @@ struct GemmP {
   const float* rowbias; int rpg; long rb_ld;
   float alpha;
   int M, N, K, Kvalid;
-  int geglu;
+  int geglu, silu;
   // convolution (A gathered from NHWC x)
   int conv, IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
 };
@@ -171,6 +171,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmP p) {
           if (p.bias) v += p.bias[n];
           if (rbrow) v += rbrow[n];
           if (p.R) v += (float)p.R[rbz + (long)m * p.ldr + n];
+          if (p.silu) v = silu_f(v);
           if (p.c_f32)
             ((float*)p.C)[cb + (long)m * p.ldc + n] = v;
           else
@@ -238,6 +239,7 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.alpha = a->alpha;
   p.M = a->M; p.N = a->N; p.K = (a->K + 31) / 32 * 32; p.Kvalid = a->K;
   p.geglu = a->epilogue == RDMI_EPI_GEGLU;
+  p.silu = a->epilogue == RDMI_EPI_SILU;
   return launch(p, a->batch, (hipStream_t)stream, p.geglu);
 }
 
@@ -252,7 +254,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   p.A = (const f16*)a->x; p.Wt = (const f16*)a->w; p.ldw = a->Kp;
   p.C = a->y; p.ldc = a->y_ld > 0 ? a->y_ld : a->Cout;
   p.bias = a->bias; p.R = (const f16*)a->residual; p.ldr = a->res_ld > 0 ? a->res_ld : a->Cout;
-  p.rowbias = a->rowbias; p.rpg = a->Ho * a->Wo; p.rb_ld = a->Cout;
+  p.rowbias = a->rowbias; p.rpg = a->Ho * a->Wo; p.rb_ld = a->rowbias_ld;
   p.alpha = a->alpha;
   p.M = a->B * a->Ho * a->Wo; p.N = a->Cout; p.K = a->Kp; p.Kvalid = K;
   p.conv = 1; p.IH = a->H; p.IW = a->W; p.Cin = a->Cin; p.Ho = a->Ho; p.Wo = a->Wo;

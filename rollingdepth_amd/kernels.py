@@ -76,7 +76,7 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> torch.T
 def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
          bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
          rowbias: Optional[torch.Tensor] = None, rows_per_group: int = 0, alpha: float = 1.0,
-         geglu: bool = False, out_f32: bool = False, n: Optional[int] = None) -> torch.Tensor:
+         geglu: bool = False, out_f32: bool = False, n: Optional[int] = None, silu: bool = False) -> torch.Tensor:
     """out[m, :] = alpha·a[m, :k] @ w[:, :k]ᵀ + bias (+ rowbias[m // rows_per_group]) (+ residual).
     a: f16 [..., M, lda]; w: f16 [N, Kp]; batched over a leading dim when a is 3-D."""
     _need(a, F16, "gemm.a")
@@ -89,6 +89,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
         shape = (batch, M, NO) if a.dim() == 3 else (M, NO)
         out = torch.empty(shape, dtype=F32 if out_f32 else F16, device=a.device)
     g = _gemm_args(a, w, out, bias, residual, rowbias, rows_per_group, alpha, M, N, k, batch, geglu, out_f32)
+    if silu:
+        g.epilogue = 2
     check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
     return out
 
@@ -143,6 +145,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     a.y_ld = out.stride(-2)
     a.res_ld = residual.stride(-2) if residual is not None else 0
     a.alpha = alpha
+    a.rowbias_ld = 0 if (rowbias is not None and rowbias.dim() == 1) else (rowbias.stride(0) if rowbias is not None else 0)
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
     check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")

@@ -1,0 +1,314 @@
+"""RollingDepthPipeline — the reference's call surface (rollingdepth/rollingdepth_pipeline.py:52-740)
+over the librdmi HIP path.
+
+What stays exactly the reference's: argument names/defaults and checks of `forward` (:193-258),
+dilation capping (:504-515, including its gap-vs-dilation comparison), snippet indices (:465-502),
+the shared init noise broadcast to every frame (:282-288), rgb-latent-first channel concat
+(:646-651), 1-step DDIM, decode + channel mean (:706-740), DepthAligner co-alignment and the
+min/max renormalisation (:306-318), output layout (:345-353), and the in-place mutation of the
+caller's `dilations` list (:246-252).
+
+What is the build's own: snippets of a dilation are batched `snippet_batch` at a time through
+one UNet call (the reference's processor only supports b = 1 per call; batching is
+legal because each snippet's attention fold is independent), frames are encoded/decoded
+`vae_batch` at a time, activations are NHWC f16 on the device, and nothing syncs with the host
+until the outputs are copied back.  `init_noise` may be injected for parity runs (the reference
+draws it from the device RNG).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Union
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .aligner import DepthAligner
+from .config import RD_SCHEDULER, SD2_UNET, SD2_VAE
+from .scheduler import DDIMScheduler
+from .unet import UNet
+from .vae import VAE
+from . import weights as Wt
+
+F16, F32 = torch.float16, torch.float32
+
+
+@dataclass
+class RollingDepthOutput:
+    input_rgb: torch.Tensor
+    depth_pred: torch.Tensor
+    snippet_ls: Optional[List[torch.Tensor]]
+    depth_coaligned: Optional[torch.Tensor]
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+def _load_state_dict(path: str) -> Dict[str, torch.Tensor]:
+    from safetensors.torch import load_file
+
+    for name in ("diffusion_pytorch_model.safetensors", "model.safetensors"):
+        p = os.path.join(path, name)
+        if os.path.exists(p):
+            return {k: v.float() for k, v in load_file(p).items()}
+    p = os.path.join(path, "diffusion_pytorch_model.bin")
+    if os.path.exists(p):
+        return {k: v.float() for k, v in torch.load(p, map_location="cpu", weights_only=True).items()}
+    raise FileNotFoundError(f"no weights under {path}")
+
+
+class RollingDepthPipeline:
+    rgb_latent_scale_factor = 0.18215
+    depth_latent_scale_factor = 0.18215
+    N_CHANNEL_PER_LATENT = 4
+
+    def __init__(self, unet: UNet, vae: VAE, scheduler: DDIMScheduler, text_encoder=None, tokenizer=None):
+        self.unet, self.vae, self.scheduler = unet, vae, scheduler
+        self.text_encoder, self.tokenizer = text_encoder, tokenizer
+        self.empty_text_embed: Optional[torch.Tensor] = None
+        self.snippet_batch = 8
+        self.vae_batch = 8
+        self._dev = unet.dev
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_pretrained(cls, path: str, torch_dtype=torch.float16, device="cuda", **kw) -> "RollingDepthPipeline":
+        """Diffusers-format checkpoint directory (model_index.json, unet/, vae/, scheduler/;
+        pipeline_utils.py:480).  Weights via safetensors (or torch.load(weights_only=True))."""
+        if torch_dtype not in (torch.float16, None):
+            raise NotImplementedError("this build runs the f16 path (f32 kernels: next round)")
+        rd = lambda sub: json.load(open(os.path.join(path, sub, "config.json" if sub != "scheduler" else "scheduler_config.json")))
+        ucfg, vcfg, scfg = rd("unet"), rd("vae"), rd("scheduler")
+        unet = UNet(ucfg, _load_state_dict(os.path.join(path, "unet")), device)
+        vae = VAE(vcfg, _load_state_dict(os.path.join(path, "vae")), device)
+        pipe = cls(unet, vae, DDIMScheduler.from_config(scfg))
+        emb = os.path.join(path, "empty_text_embed.safetensors")
+        if os.path.exists(emb):
+            from safetensors.torch import load_file
+            pipe.empty_text_embed = load_file(emb)["embed"]
+        return pipe
+
+    @classmethod
+    def from_synthetic(cls, unet_cfg=SD2_UNET, vae_cfg=SD2_VAE, sched_cfg=RD_SCHEDULER, seed: int = 0,
+                       device="cuda") -> "RollingDepthPipeline":
+        """Random-init weights of the architecture (no checkpoint in the image), deterministic
+        per state-dict key (weights.py) — identical to what the golden fixtures used."""
+        unet = UNet(unet_cfg, Wt.synth_state_dict(Wt.unet_param_shapes(unet_cfg), seed), device)
+        vae = VAE(vae_cfg, Wt.synth_state_dict(Wt.vae_param_shapes(vae_cfg), seed), device)
+        pipe = cls(unet, vae, DDIMScheduler.from_config(sched_cfg))
+        pipe.empty_text_embed = Wt.synth_context(unet_cfg["cross_attention_dim"], seed)
+        return pipe
+
+    @property
+    def device(self) -> torch.device:
+        return self._dev
+
+    @property
+    def dtype(self):
+        return F16
+
+    def to(self, device):
+        if torch.device(device) != self._dev:
+            raise NotImplementedError("construct the pipeline on its target device")
+        return self
+
+    def encode_empty_text(self):
+        """rollingdepth_pipeline.py:178-191 — needs the CLIP text encoder; the build caches the
+        constant [1, 2, 1024] embedding instead (set `empty_text_embed`)."""
+        if self.text_encoder is None or self.tokenizer is None:
+            raise RuntimeError("empty_text_embed not set and no text encoder available")
+        ids = self.tokenizer("", padding="do_not_pad", max_length=self.tokenizer.model_max_length, truncation=True,
+                             return_tensors="pt").input_ids
+        with torch.no_grad():
+            self.empty_text_embed = self.text_encoder(ids)[0].float()
+
+    # ------------------------------------------------------------------ reference helpers
+    @staticmethod
+    def get_snippet_indice(i_step: int, timesteps, seq_len: int, snippet_len: int, dilation_start: int,
+                           dilation_end: int, stride: int) -> List[List[int]]:
+        gap_start, gap_end = dilation_start - 1, dilation_end - 1
+        assert gap_start >= gap_end, f"expect gap_start > gap_end, but got {gap_start} and {gap_end}"
+        assert gap_start >= 0 and gap_end >= 0
+        total = len(timesteps)
+        gap = int((1 - i_step / total) * (gap_start - gap_end) + gap_end)
+        win = (snippet_len - 1) * (gap + 1) + 1
+        starts = list(range(0, seq_len - win + 1, stride))
+        if starts[-1] < seq_len - win:
+            starts.append(seq_len - win)
+        idx = [list(range(s, s + win, gap + 1)) for s in starts]
+        if set(range(seq_len)) != {x for f in idx for x in f}:
+            logging.warning("Not every frame is covered. Consider reducing dilation for short videos")
+        return idx
+
+    @staticmethod
+    def cap_max_dilation(seq_len: int, snippet_len: int, dilation: int, verbose: bool = False) -> int:
+        max_gap = int(seq_len / snippet_len) - 1
+        if max_gap < dilation:
+            (logging.info if verbose else logging.debug)(
+                f"dilation = {dilation} is too big for {seq_len} frames. Reduced to {max_gap}")
+            dilation = min(max_gap, dilation)
+        return dilation
+
+    # ------------------------------------------------------------------ stages
+    def encode_rgb(self, frames_nchw: torch.Tensor) -> torch.Tensor:
+        """[N,3,H,W] in [-1,1] (any float dtype, on device) → NHWC f16 [N, h, w, 8] latents·0.18215."""
+        N, _, H, W = frames_nchw.shape
+        f = self.vae.factor
+        out = torch.zeros((N, H // f, W // f, self.vae.lat_pad), dtype=F16, device=self.device)
+        for i in range(0, N, self.vae_batch):
+            x = K.nchw_to_nhwc(frames_nchw[i:i + self.vae_batch], self.vae.in_pad)
+            self.vae.encode(x, out=out[i:i + self.vae_batch])
+        return out
+
+    def decode_depth(self, z_scaled: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """z_scaled: NHWC [B, h, w, 8] already divided by 0.18215 → out [B, H, W, 1] depth."""
+        for i in range(0, z_scaled.shape[0], self.vae_batch):
+            self.vae.decode_depth(z_scaled[i:i + self.vae_batch], out=out[i:i + self.vae_batch])
+        return out
+
+    def _context(self) -> torch.Tensor:
+        if self.empty_text_embed is None:
+            self.encode_empty_text()
+        ctx = self.empty_text_embed
+        if getattr(self, "_ctx16_src", None) is not ctx:
+            self._ctx16 = ctx.to(self.device, F16).contiguous()
+            self._ctx16_src = ctx
+            self.unet.set_context(self._ctx16)
+        return self._ctx16
+
+    def init_snippet_infer(self, rgb_latent: torch.Tensor, init_noise: torch.Tensor, dilations: List[int],
+                           snippet_lengths: List[int], init_infer_steps: List[int], strides: List[int],
+                           snippet_subset=None, record: Optional[dict] = None) -> List[torch.Tensor]:
+        """rollingdepth_pipeline.py:356-463 with snippets batched per UNet call.
+        rgb_latent NHWC [N,h,w,8]; init_noise NHWC [1,h,w,8].  Returns per dilation the decoded
+        snippets [n_d, w, H, W] f16 (device).  `snippet_subset[d]` (optional) restricts the work
+        to those snippet indices (multi-GPU sharding); other rows are left uninitialised."""
+        self._context()
+        N, h, w, _ = rgb_latent.shape
+        H, W = h * self.vae.factor, w * self.vae.factor
+        outs = []
+        for di, (dil, slen, stride, steps) in enumerate(zip(dilations, snippet_lengths, strides, init_infer_steps)):
+            self.scheduler.set_timesteps(steps)
+            timesteps = self.scheduler.timesteps
+            idx = self.get_snippet_indice(0, timesteps, N, slen, dil, dil, stride)
+            buf = torch.empty((len(idx), slen, H, W), dtype=F16, device=self.device)
+            todo = list(range(len(idx))) if snippet_subset is None else list(snippet_subset[di])
+            for b0 in range(0, len(todo), self.snippet_batch):
+                sel = todo[b0:b0 + self.snippet_batch]
+                fidx = torch.tensor([f for s in sel for f in idx[s]], dtype=torch.int32, device=self.device)
+                x = K.gather_unet_input(rgb_latent, init_noise, fidx, depth_bcast=True)
+                depth_view = x[..., 4:8]
+                for si, t in enumerate(timesteps.tolist()):
+                    pred = self.unet.forward(x, int(t), num_view=slen)
+                    last = si == len(timesteps) - 1
+                    if last:
+                        zin = self.scheduler.step_(pred, int(t), depth_view, 1.0 / self.depth_latent_scale_factor,
+                                                   channels=self.N_CHANNEL_PER_LATENT,
+                                                   out=torch.empty((x.shape[0], h, w, 8), dtype=F16,
+                                                                   device=self.device))
+                        if record is not None:
+                            record.setdefault("unet_out", []).append(pred)
+                            record.setdefault("snippet_latent", []).append(
+                                self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4,
+                                                     out=torch.empty((x.shape[0], h, w, 8), dtype=F16,
+                                                                     device=self.device)))
+                    else:
+                        x2 = x.clone()
+                        self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4, out=x2[..., 4:])
+                        x = x2
+                        depth_view = x[..., 4:8]
+                dec = buf[sel[0]:sel[-1] + 1] if sel == list(range(sel[0], sel[-1] + 1)) else None
+                tgt = torch.empty((len(sel) * slen, H, W, 1), dtype=F16, device=self.device) if dec is None \
+                    else dec.view(len(sel) * slen, H, W, 1)
+                self.decode_depth(zin, tgt)
+                if dec is None:
+                    buf[torch.tensor(sel, device=self.device)] = tgt.view(len(sel), slen, H, W)
+            outs.append(buf)
+        return outs
+
+    # ------------------------------------------------------------------ entry points
+    @torch.no_grad()
+    def __call__(self, input_video_path, start_frame: int = 0, frame_count: int = 0, processing_res: int = 1024,
+                 resample_method: str = "BILINEAR", dilations: List[int] = [1, 25], cap_dilation: bool = True,
+                 snippet_lengths: List[int] = [3], init_infer_steps: List[int] = [1], strides: List[int] = [1],
+                 coalign_kwargs: Union[Dict, None] = None, refine_step: int = 0, refine_snippet_len: int = 3,
+                 refine_start_dilation: int = 6, generator: Union[torch.Generator, None] = None,
+                 verbose: bool = False, max_vae_bs: int = 4, unload_snippet: bool = False,
+                 restore_res: bool = False, input_fg_video_path=None, **kw) -> RollingDepthOutput:
+        """rollingdepth_pipeline.py:78-176.  Accepts a [N,3,H,W] tensor in [-1,1] in place of a
+        video path (video decoding needs PyAV, absent from this image)."""
+        src = input_fg_video_path if input_fg_video_path is not None else input_video_path
+        if isinstance(src, torch.Tensor):
+            frames = src
+        else:
+            from .video_io import load_video_frames
+            frames, _ = load_video_frames(src, start_frame, frame_count, processing_res, resample_method, verbose)
+        if restore_res:
+            raise NotImplementedError("restore_res needs torchvision resize (absent from this image)")
+        return self.forward(frames[None] if frames.dim() == 4 else frames, dilations, cap_dilation, snippet_lengths,
+                            init_infer_steps, strides, coalign_kwargs, refine_step, refine_snippet_len,
+                            refine_start_dilation, generator, verbose, max_vae_bs, unload_snippet, **kw)
+
+    @torch.no_grad()
+    def forward(self, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool,
+                snippet_lengths: List[int], init_infer_steps: List[int], strides: List[int],
+                coalign_kwargs: Union[Dict, None], refine_step: int, refine_snippet_len: int,
+                refine_start_dilation: int, generator: Union[torch.Generator, None], verbose: bool,
+                max_vae_bs: int, unload_snippet: bool, init_noise: Optional[torch.Tensor] = None,
+                record: Optional[dict] = None) -> RollingDepthOutput:
+        # ----------------- checks (rollingdepth_pipeline.py:214-252)
+        assert 1 in dilations, "dilations should include 1"
+        assert len(snippet_lengths) == len(set(snippet_lengths)), f"Repeated values found in {snippet_lengths = }"
+        if len(snippet_lengths) > 1:
+            assert len(snippet_lengths) == len(dilations)
+        else:
+            snippet_lengths = snippet_lengths * len(dilations)
+        if len(init_infer_steps) > 1:
+            assert len(init_infer_steps) == len(dilations)
+        else:
+            init_infer_steps = init_infer_steps * len(dilations)
+        assert min(init_infer_steps) > 0, "Minimum inference step is 1"
+        if len(strides) > 1:
+            assert len(strides) == len(dilations)
+        else:
+            strides = strides * len(dilations)
+        if [1] * len(dilations) != strides:
+            raise NotImplementedError("Only implemented for stride 1")
+        seq_len = input_frames.shape[1]
+        if cap_dilation:
+            for i, d in enumerate(dilations):
+                dilations[i] = self.cap_max_dilation(seq_len, snippet_lengths[i], d, verbose)
+            refine_start_dilation = self.cap_max_dilation(seq_len, refine_snippet_len, refine_start_dilation, verbose)
+        if refine_step > 0:
+            raise NotImplementedError("refine (full/paper presets) is the next row (SURVEY.md §8f rank 1)")
+        if input_frames.shape[0] != 1:
+            raise NotImplementedError("Layered inference is only implemented for B=1")
+        # ----------------- encode (H2D boundary :263)
+        frames = input_frames[0].to(self.device)
+        rgb_latent = self.encode_rgb(frames)
+        N, h, w, _ = rgb_latent.shape
+        # ----------------- shared init noise (:282-288)
+        if init_noise is None:
+            init_noise = torch.randn((1, 4, h, w), device=self.device, dtype=F16, generator=generator)
+        noise = K.nchw_to_nhwc(init_noise.to(self.device), 8)
+        snippets = self.init_snippet_infer(rgb_latent, noise, dilations, snippet_lengths, init_infer_steps, strides,
+                                           record=record)
+        # ----------------- co-alignment + renormalisation (:306-318)
+        aligner = DepthAligner(device=self.device, verbose=verbose, **(coalign_kwargs or {}))
+        H, W = snippets[0].shape[-2:]
+        merged, scales, trans, hist = aligner.run([s.view(s.shape[0], s.shape[1], 1, H, W) for s in snippets],
+                                                  dilations)
+        d = merged.float().contiguous()
+        K.renormalize_(d, K.minmax(d))
+        depth = d.to(F16)
+        if record is not None:
+            record.update(rgb_latent=rgb_latent, scales=scales, translations=trans, loss_history=hist,
+                          dilations=list(dilations))
+        # ----------------- outputs (:345-353, D2H boundary)
+        snip_out = [s.view(s.shape[0], s.shape[1], 1, H, W).cpu() for s in snippets]
+        return RollingDepthOutput(input_rgb=input_frames[0].float().cpu() / 2.0 + 0.5, depth_pred=depth.cpu(),
+                                  snippet_ls=snip_out, depth_coaligned=depth.cpu())

@@ -1,0 +1,277 @@
+"""UNet2DConditionModel forward on librdmi (NHWC f16 activations, f32 accumulation).
+
+Mirrors diffusers/models/unets/unet_2d_condition.py:1039-1324 with RollingDepth's `num_view`
+threading (:1226-1301 → Transformer2DModel → BasicTransformerBlock → Attention with the
+cross-frame fold, attention_processor.py:2208-2266).  Weights come from a diffusers state dict
+(same keys as the reference) and are packed once at construction:
+  * convs → [Cout][kh][kw][Cin_pad] f16 (implicit-GEMM K order), biases f32;
+  * attn1 to_q/to_k/to_v fused into one [3C, C] projection (one GEMM, one read of the input);
+  * attn2 K/V of the constant empty-text context are projected once per context
+    (rollingdepth_pipeline.py:271-272,376: the context never changes);
+  * GEGLU proj rows interleaved for the fused GEGLU epilogue;
+  * all ResnetBlock2D.time_emb_proj rows concatenated: the time embedding of a timestep is one
+    GEMM chain, cached per timestep (every 1-step snippet uses t = 999).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from .config import unet_heads
+
+F16, F32 = torch.float16, torch.float32
+
+
+def _sinusoid(t: int, dim: int, flip: bool, shift: float) -> np.ndarray:
+    """Timesteps projection (embeddings.py:591 / get_timestep_embedding) for one integer t —
+    a constant table lookup computed once per timestep value, like a positional table."""
+    half = dim // 2
+    ex = -math.log(10000) * np.arange(half, dtype=np.float32) / (half - shift)
+    e = np.float32(t) * np.exp(ex.astype(np.float32)).astype(np.float32)
+    e = np.concatenate([np.sin(e), np.cos(e)]).astype(np.float32)
+    if flip:
+        e = np.concatenate([e[half:], e[:half]])
+    return e
+
+
+class _Lin:
+    def __init__(self, sd, key, dev, bias=True):
+        w = sd[key + ".weight"]
+        self.n, self.k = w.shape
+        self.w = K.pack_linear(w, dev)
+        self.b = sd[key + ".bias"].to(dev, F32) if bias and key + ".bias" in sd else None
+
+    def __call__(self, x, out=None, residual=None, silu=False):
+        return K.gemm(x, self.w, self.k, out=out, bias=self.b, residual=residual, silu=silu)
+
+
+class _Conv:
+    def __init__(self, sd, key, dev, stride=1, pad=1):
+        w = sd[key + ".weight"]
+        self.cout, self.cin, self.k, _ = w.shape
+        self.cin_pad = K.pad_channels(self.cin)
+        self.w = K.pack_conv(w, dev, self.cin_pad)
+        self.b = sd[key + ".bias"].to(dev, F32) if key + ".bias" in sd else None
+        self.stride, self.pad = stride, pad
+
+    def __call__(self, x, upsample=False, residual=None, rowbias=None, out=None, pad_tl=None, out_hw=None):
+        return K.conv2d(x, self.w, self.cout, self.k, stride=self.stride, pad=self.pad, pad_tl=pad_tl,
+                        upsample=upsample, bias=self.b, residual=residual, rowbias=rowbias, out=out, out_hw=out_hw)
+
+
+class _Norm:
+    def __init__(self, sd, key, dev):
+        self.g = sd[key + ".weight"].to(dev, F32)
+        self.b = sd[key + ".bias"].to(dev, F32)
+
+
+class Resnet:
+    """ResnetBlock2D (resnet.py:189, forward :320-373)."""
+
+    def __init__(self, sd, p, dev, groups, eps, temb_slot=None):
+        self.n1 = _Norm(sd, p + ".norm1", dev)
+        self.c1 = _Conv(sd, p + ".conv1", dev)
+        self.n2 = _Norm(sd, p + ".norm2", dev)
+        self.c2 = _Conv(sd, p + ".conv2", dev)
+        self.sc = _Conv(sd, p + ".conv_shortcut", dev, pad=0) if p + ".conv_shortcut.weight" in sd else None
+        self.groups, self.eps = groups, eps
+        self.temb_slot = temb_slot  # (offset, width) into the concatenated time projections
+
+    def __call__(self, x, temb_all=None):
+        h = K.groupnorm(x, self.n1.g, self.n1.b, self.groups, self.eps, silu=True)
+        rb = None
+        if self.temb_slot is not None and temb_all is not None:
+            o, w = self.temb_slot
+            rb = temb_all[o:o + w]
+        h = self.c1(h, rowbias=rb)
+        h = K.groupnorm(h, self.n2.g, self.n2.b, self.groups, self.eps, silu=True)
+        res = self.sc(x) if self.sc is not None else x
+        return self.c2(h, residual=res)
+
+
+class Transformer:
+    """Transformer2DModel (use_linear_projection) + BasicTransformerBlock with the modified
+    cross-frame attn1 (num_view fold) and attn2 against the constant context."""
+
+    def __init__(self, sd, p, dev, heads, groups):
+        self.heads, self.groups = heads, groups
+        self.norm = _Norm(sd, p + ".norm", dev)
+        self.proj_in = _Lin(sd, p + ".proj_in", dev)
+        self.proj_out = _Lin(sd, p + ".proj_out", dev)
+        q = p + ".transformer_blocks.0"
+        self.ln1 = _Norm(sd, q + ".norm1", dev)
+        self.ln2 = _Norm(sd, q + ".norm2", dev)
+        self.ln3 = _Norm(sd, q + ".norm3", dev)
+        wqkv = torch.cat([sd[f"{q}.attn1.to_{n}.weight"] for n in ("q", "k", "v")], 0)
+        self.c = wqkv.shape[1]
+        self.qkv = K.pack_linear(wqkv, dev)
+        self.o1 = _Lin(sd, q + ".attn1.to_out.0", dev)
+        self.q2 = _Lin(sd, q + ".attn2.to_q", dev, bias=False)
+        self.k2 = _Lin(sd, q + ".attn2.to_k", dev, bias=False)
+        self.v2 = _Lin(sd, q + ".attn2.to_v", dev, bias=False)
+        self.o2 = _Lin(sd, q + ".attn2.to_out.0", dev)
+        wp, bp = K.geglu_permute(sd[q + ".ff.net.0.proj.weight"], sd[q + ".ff.net.0.proj.bias"])
+        self.ff1_w = K.pack_linear(wp, dev)
+        self.ff1_b = bp.to(dev, F32)
+        self.ff2 = _Lin(sd, q + ".ff.net.2", dev)
+        self._ctx_key = None
+
+    def set_context(self, ctx16: torch.Tensor):
+        """K/V of attn2 for the (constant) encoder_hidden_states [Bc, L, Dctx] f16."""
+        if self._ctx_key is ctx16:
+            return
+        self.k2c = K.gemm(ctx16, self.k2.w, self.k2.k)
+        self.v2c = K.gemm(ctx16, self.v2.w, self.v2.k)
+        self._ctx_key = ctx16
+
+    def __call__(self, x, num_view: Optional[int]):
+        B, H, W, C = x.shape
+        HW = H * W
+        t = K.groupnorm(x, self.norm.g, self.norm.b, self.groups, 1e-6, silu=False)
+        t = self.proj_in(t.view(B * HW, C))
+        # attn1: cross-frame self-attention over the snippet's n·h·w tokens
+        n1 = K.layernorm(t, self.ln1.g, self.ln1.b, 1e-5)
+        qkv = K.gemm(n1, self.qkv, C)
+        nv = num_view or 1
+        bb = B // nv
+        qkv3 = qkv.view(bb, nv * HW, 3 * C)
+        o = K.attention(qkv3[..., :C], qkv3[..., C:2 * C], qkv3[..., 2 * C:], self.heads)
+        t = self.o1(o.view(B * HW, C), residual=t)
+        # attn2: cross-attention to the context (the fold is a no-op for shared K/V)
+        n2 = K.layernorm(t, self.ln2.g, self.ln2.b, 1e-5)
+        q2 = self.q2(n2)
+        kv_b = self.k2c.shape[0]
+        if kv_b == 1:
+            o2 = K.attention_smallkv(q2.view(1, B * HW, C), self.k2c, self.v2c, self.heads)
+        else:
+            o2 = K.attention_smallkv(q2.view(kv_b, -1, C), self.k2c, self.v2c, self.heads)
+        t = self.o2(o2.view(B * HW, C), residual=t)
+        # GEGLU feed-forward
+        n3 = K.layernorm(t, self.ln3.g, self.ln3.b, 1e-5)
+        f = K.gemm(n3, self.ff1_w, C, bias=self.ff1_b, geglu=True)
+        t = self.ff2(f, residual=t)
+        out = self.proj_out(t, residual=x.view(B * HW, C))
+        return out.view(B, H, W, C)
+
+
+class UNet:
+    """Native UNet2DConditionModel (SD2 family: CrossAttnDown* + Down, mid CrossAttn, Up + CrossAttnUp*)."""
+
+    def __init__(self, cfg: dict, sd: Dict[str, torch.Tensor], device):
+        dev = torch.device(device)
+        self.cfg, self.dev = cfg, dev
+        g, eps = cfg["norm_num_groups"], cfg["norm_eps"]
+        heads = unet_heads(cfg)
+        ch = cfg["block_out_channels"]
+        L = cfg["layers_per_block"]
+        self.ch, self.L = ch, L
+        self.in_ch = cfg["in_channels"]
+        self.out_ch = cfg["out_channels"]
+        self.conv_in = _Conv(sd, "conv_in", dev)
+        self.t1 = _Lin(sd, "time_embedding.linear_1", dev)
+        self.t2 = _Lin(sd, "time_embedding.linear_2", dev)
+        # concatenated time_emb_proj of every resnet
+        tp_w, tp_b, off = [], [], 0
+        slots = {}
+        for k in sd:
+            if k.endswith("time_emb_proj.weight"):
+                p = k[: -len(".time_emb_proj.weight")]
+                w = sd[k]
+                tp_w.append(w)
+                tp_b.append(sd[p + ".time_emb_proj.bias"])
+                slots[p] = (off, w.shape[0])
+                off += w.shape[0]
+        self.tp_w = K.pack_linear(torch.cat(tp_w, 0), dev)
+        self.tp_b = torch.cat(tp_b, 0).to(dev, F32)
+        self.tp_k = tp_w[0].shape[1]
+        self._temb_cache = {}
+
+        def R(p):
+            return Resnet(sd, p, dev, g, eps, slots.get(p))
+
+        self.down = []
+        for i, bt in enumerate(cfg["down_block_types"]):
+            blk = {"res": [], "attn": [], "ds": None}
+            for j in range(L):
+                blk["res"].append(R(f"down_blocks.{i}.resnets.{j}"))
+                if bt == "CrossAttnDownBlock2D":
+                    blk["attn"].append(Transformer(sd, f"down_blocks.{i}.attentions.{j}", dev, heads[i], g))
+            if i < len(ch) - 1:
+                blk["ds"] = _Conv(sd, f"down_blocks.{i}.downsamplers.0.conv", dev, stride=2, pad=1)
+            self.down.append(blk)
+        self.mid_res = [R("mid_block.resnets.0"), R("mid_block.resnets.1")]
+        self.mid_attn = Transformer(sd, "mid_block.attentions.0", dev, heads[-1], g)
+        rheads = list(reversed(heads))
+        self.up = []
+        for i, bt in enumerate(cfg["up_block_types"]):
+            blk = {"res": [], "attn": [], "us": None}
+            for j in range(L + 1):
+                blk["res"].append(R(f"up_blocks.{i}.resnets.{j}"))
+                if bt == "CrossAttnUpBlock2D":
+                    blk["attn"].append(Transformer(sd, f"up_blocks.{i}.attentions.{j}", dev, rheads[i], g))
+            if i < len(ch) - 1:
+                blk["us"] = _Conv(sd, f"up_blocks.{i}.upsamplers.0.conv", dev)
+            self.up.append(blk)
+        self.norm_out = _Norm(sd, "conv_norm_out", dev)
+        self.conv_out = _Conv(sd, "conv_out", dev)
+        self.groups, self.eps = g, eps
+        self.transformers = [t for b in self.down for t in b["attn"]] + [self.mid_attn] + \
+                            [t for b in self.up for t in b["attn"]]
+
+    # ------------------------------------------------------------------ time embedding
+    def time_embedding(self, t: int) -> torch.Tensor:
+        """silu(TimestepEmbedding(Timesteps(t))) projected through every resnet's time_emb_proj
+        (resnet.py:338-343), cached per timestep value; [Σ Cout] f32 on device."""
+        e = self._temb_cache.get(int(t))
+        if e is not None:
+            return e
+        s = _sinusoid(int(t), self.ch[0], self.cfg.get("flip_sin_to_cos", True), self.cfg.get("freq_shift", 0))
+        x = torch.from_numpy(s).to(self.dev, F16).view(1, -1)
+        h = K.gemm(x, self.t1.w, self.t1.k, bias=self.t1.b, silu=True)
+        emb = K.gemm(h, self.t2.w, self.t2.k, bias=self.t2.b, silu=True)  # silu(temb) feeds every proj
+        proj = K.gemm(emb, self.tp_w, self.tp_k, bias=self.tp_b, out_f32=True)
+        e = proj.view(-1)
+        self._temb_cache[int(t)] = e
+        return e
+
+    def set_context(self, ctx16: torch.Tensor):
+        for tr in self.transformers:
+            tr.set_context(ctx16)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, sample: torch.Tensor, t: int, num_view: Optional[int]) -> torch.Tensor:
+        """sample: NHWC f16 [B, h, w, in_ch_pad]; one timestep value for the whole batch (the
+        pipeline repeats a scalar t, rollingdepth_pipeline.py:434).  Returns NHWC [B, h, w, out]."""
+        B, h, w, _ = sample.shape
+        f = 2 ** (len(self.ch) - 1)
+        if h % f or w % f:
+            raise NotImplementedError(f"latent {h}x{w} not a multiple of {f} (forward_upsample_size path)")
+        temb = self.time_embedding(t)
+        x = self.conv_in(sample)
+        skips = [x]
+        for blk in self.down:
+            for j, r in enumerate(blk["res"]):
+                x = r(x, temb)
+                if blk["attn"]:
+                    x = blk["attn"][j](x, num_view)
+                skips.append(x)
+            if blk["ds"] is not None:
+                x = blk["ds"](x)
+                skips.append(x)
+        x = self.mid_res[0](x, temb)
+        x = self.mid_attn(x, num_view)
+        x = self.mid_res[1](x, temb)
+        for blk in self.up:
+            for j, r in enumerate(blk["res"]):
+                x = K.concat_channels(x, skips.pop())
+                x = r(x, temb)
+                if blk["attn"]:
+                    x = blk["attn"][j](x, num_view)
+            if blk["us"] is not None:
+                x = blk["us"](x, upsample=True)
+        x = K.groupnorm(x, self.norm_out.g, self.norm_out.b, self.groups, self.eps, silu=True)
+        return self.conv_out(x)
