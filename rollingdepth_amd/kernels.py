@@ -19,6 +19,49 @@ def _stream() -> int:
     return torch.cuda.current_stream().cuda_stream
 
 
+# ----------------------------------------------------------------------------- live kernel timing
+# bench.py brackets the hot kernels with HIP events on the launch stream (no host sync inside the
+# timed region) to compute per-kernel achieved TFLOP/s.
+_PROF = None
+
+
+def profile_start():
+    global _PROF
+    _PROF = {}
+
+
+def profile_stop():
+    global _PROF
+    prof, _PROF = _PROF, None
+    if not prof:
+        return {}
+    torch.cuda.synchronize()
+    out = {}
+    for name, recs in prof.items():
+        ms = sum(a.elapsed_time(b) for a, b, _ in recs)
+        out[name] = {"ms": ms, "flop": float(sum(f for _, _, f in recs)), "n": len(recs)}
+    return out
+
+
+class _Timed:
+    __slots__ = ("name", "flop", "ev")
+
+    def __init__(self, name, flop):
+        self.name, self.flop, self.ev = name, flop, None
+
+    def __enter__(self):
+        if _PROF is not None:
+            self.ev = torch.cuda.Event(enable_timing=True)
+            self.ev.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _PROF is not None and self.ev is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _PROF.setdefault(self.name, []).append((self.ev, e, self.flop))
+
+
 def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
@@ -91,7 +134,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     g = _gemm_args(a, w, out, bias, residual, rowbias, rows_per_group, alpha, M, N, k, batch, geglu, out_f32)
     if silu:
         g.epilogue = 2
-    check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
+    with _Timed("implicit_gemm", 2.0 * M * N * k * batch):
+        check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
     return out
 
 
@@ -148,7 +192,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     a.rowbias_ld = 0 if (rowbias is not None and rowbias.dim() == 1) else (rowbias.stride(0) if rowbias is not None else 0)
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
-    check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
+    with _Timed("implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin):
+        check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
     return out
 
 
@@ -212,9 +257,10 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
     if out is None:
         out = torch.empty((B, Sq, HD), dtype=F16, device=q.device)
     sc = 1.0 / math.sqrt(D) if scale is None else scale
-    check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
-                                 q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
-                                 v.stride(0), out.stride(0), sc, _stream()), "rdmi_attention_fwd")
+    with _Timed("attention_fwd", 4.0 * B * heads * Sq * Sk * D):
+        check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
+                                     q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
+                                     v.stride(0), out.stride(0), sc, _stream()), "rdmi_attention_fwd")
     return out
 
 

@@ -23,8 +23,10 @@ def _synth(N=14, dil=(1, 3), H=40, W=44, seed=0, dtype=np.float32):
     return out, list(dil)
 
 
-@pytest.mark.parametrize("iters", [1, 50, 400])
+@pytest.mark.parametrize("iters", [1, 50, 150])
 def test_aligner_optimize_matches_oracle(iters):
+    """Before Adam reaches its oscillating L1 regime (~200-300 it) the trajectories agree to f32
+    rounding: parameters to 2e-5·(iters/50), loss history to 1e-5 relative."""
     from rollingdepth_amd.aligner import DepthAligner
 
     snips, dil = _synth()
@@ -34,8 +36,32 @@ def test_aligner_optimize_matches_oracle(iters):
     for d in range(len(dil)):
         assert np.abs(s[d].cpu().numpy().ravel() - ref_s[d]).max() < 2e-5 * max(1, iters / 50)
         assert np.abs(t[d].cpu().numpy().ravel() - ref_t[d]).max() < 2e-5 * max(1, iters / 50)
-    assert abs(h[0][0] - ref_h[0][0]) < 1e-5 * abs(ref_h[0][0]) + 1e-7
+    np.testing.assert_allclose(np.array(h)[:, 0], np.array(ref_h)[:, 0], rtol=1e-5)
     assert np.abs(m.cpu().numpy() - ref_m).max() < 1e-4
+
+
+def test_aligner_2000_iterations_vs_reference_golden():
+    """Full 2000-iteration run on the reference's own aligner fixture (DepthAligner.run output),
+    with the tolerances of tests/test_oracle_golden.py::test_aligner_oracle_vs_reference."""
+    import json
+    import os
+    from safetensors.torch import load_file
+    from rollingdepth_amd.aligner import DepthAligner
+
+    g = os.path.join(os.path.dirname(__file__), "golden")
+    t = load_file(os.path.join(g, "aligner.safetensors"))
+    dil = json.load(open(os.path.join(g, "aligner.json")))["dilations"]
+    al = DepthAligner(device=torch.device(DEV), num_iterations=2000)
+    m, s, tr, h = al.run([t[f"snippet_{i}"].to(DEV) for i in range(len(dil))], list(dil))
+    ref_h = t["loss_hist"].numpy()
+    np.testing.assert_allclose(np.array(h)[:200, 0], ref_h[:200, 0], rtol=1e-5)
+    for i in range(len(dil)):
+        np.testing.assert_allclose(s[i].cpu().numpy().ravel(), t[f"scale_{i}"].numpy().ravel(), atol=1e-2)
+        np.testing.assert_allclose(tr[i].cpu().numpy().ravel(), t[f"trans_{i}"].numpy().ravel(), atol=1e-2)
+    ref_m = t["merged"].numpy()
+    rng = ref_m.max() - ref_m.min()
+    err = np.abs(m.cpu().numpy() - ref_m)
+    assert err.mean() <= 1e-3 * rng and err.max() <= 5e-3 * rng
 
 
 def test_aligner_merge_f16_rounding():
