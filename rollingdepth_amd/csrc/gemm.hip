@@ -12,8 +12,7 @@
 
 namespace {
 
-constexpr int BK = 32;
-constexpr int LDSK = BK + 8;  // padded LDS row (80 B) against ds_read_b128 bank conflicts
+constexpr int BK = 64;  // K per stage: 8 chunks of 8 halves (16 B) per tile row
 
 struct GemmP {
   const f16* A; long lda, sA;
@@ -26,93 +25,137 @@ struct GemmP {
   int M, N, K, Kvalid;
   int geglu, silu;
   // convolution (A gathered from NHWC x)
-  int conv, IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
+  int IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
 };
 
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmP p) {
+// MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x (kh×kw conv).
+// LDS tiles are [rows][64] halves with the 16-B chunk index XOR-swizzled by (row & 7)
+// (conflict-spread ds_read_b128 fragment reads, cdna_hip_programming.md §5.5 T2).
+template <int BM, int BN, int MODE>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int AV = BM * 4 / 256;  // 16-B A vectors per thread per K-step
-  constexpr int BV = BN * 4 / 256;
-  __shared__ __attribute__((aligned(16))) f16 lds[2][(BM + BN) * LDSK];
+  constexpr int AV = BM / 32;  // 16-B A vectors per thread per stage (8 chunks x BM rows / 256)
+  constexpr int BV = BN / 32;
+  __shared__ __attribute__((aligned(16))) f16 lds[2][(BM + BN) * BK];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int n0 = blockIdx.x * BN;
-  const int m0 = blockIdx.y * BM;
+  // XCD-aware remap (T1): dispatch id d runs on XCD d % 8; give each XCD a contiguous range of
+  // logical tiles so the n-tiles sharing one A row-panel share that XCD's L2.
+  const int nbx = gridDim.x, nby = gridDim.y;
+  const int total = nbx * nby;
+  const int bid = blockIdx.y * nbx + blockIdx.x;
+  int logical = bid;
+  if (total >= 8) {
+    const int xcd = bid & 7, q = total >> 3, r = total & 7;
+    logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int n0 = (logical % nbx) * BN;
+  const int m0 = (logical / nbx) * BM;
   const int bz = blockIdx.z;
   const f16* A = p.A + (long)bz * p.sA;
   const f16* Wt = p.Wt + (long)bz * p.sW;
 
-  const int chunk = tid & 3;
-  // per-row precompute for the A gather
-  int arow_ok[AV];
+  const int chunk = tid & 7;
+  const int rbase = tid >> 3;
+  bool arow_ok[AV];
   long abase[AV];
-  int aho[AV], awo[AV];
+  int ahb[AV], awb[AV];
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
-    int m = m0 + (tid >> 2) + 64 * i;
+    const int m = m0 + rbase + 32 * i;
     arow_ok[i] = m < p.M;
-    int mm = arow_ok[i] ? m : 0;
-    if (p.conv) {
-      int hw = p.Ho * p.Wo;
-      int b = mm / hw;
-      int r = mm - b * hw;
-      aho[i] = r / p.Wo;
-      awo[i] = r - aho[i] * p.Wo;
+    const int mm = arow_ok[i] ? m : 0;
+    if (MODE == 1) {
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int r = mm - b * hw;
+      const int ho = r / p.Wo;
+      const int wo = r - ho * p.Wo;
+      ahb[i] = ho * p.stride - p.pt;
+      awb[i] = wo * p.stride - p.pl;
       abase[i] = (long)b * p.IH * p.IW * p.Cin;
     } else {
       abase[i] = (long)mm * p.lda;
-      aho[i] = awo[i] = 0;
+      ahb[i] = awb[i] = 0;
     }
   }
+  // incremental (tap, channel-vector) of this thread's chunk: k-vector index = k0/8 + chunk
+  int tap = 0, cv = chunk;
+  if (MODE == 1) {
+    tap = chunk / p.cin_vecs;
+    cv = chunk - tap * p.cin_vecs;
+  }
+  const int Hl = p.IH << p.up, Wl = p.IW << p.up;
 
   auto loadA = [&](int k0, f16x8 (&ra)[AV]) {
     const int kk = k0 + chunk * 8;
+    const bool kok = kk < p.Kvalid;
+    if (MODE == 0) {
 #pragma unroll
-    for (int i = 0; i < AV; ++i) {
-      f16x8 v = {};
-      if (arow_ok[i] && kk < p.Kvalid) {
-        if (!p.conv) {
-          v = *(const f16x8*)(A + abase[i] + kk);
-        } else {
-          int kv = kk >> 3;
-          int tap = kv / p.cin_vecs;
-          int cv = kv - tap * p.cin_vecs;
-          int dy = tap / p.kw;
-          int dx = tap - dy * p.kw;
-          int hi = aho[i] * p.stride - p.pt + dy;
-          int wi = awo[i] * p.stride - p.pl + dx;
-          int Hl = p.IH << p.up, Wl = p.IW << p.up;
-          if (hi >= 0 && hi < Hl && wi >= 0 && wi < Wl) {
-            hi >>= p.up;
-            wi >>= p.up;
-            v = *(const f16x8*)(A + abase[i] + ((long)hi * p.IW + wi) * p.Cin + cv * 8);
-          }
-        }
+      for (int i = 0; i < AV; ++i) {
+        f16x8 v = {};
+        if (arow_ok[i] && kok) v = *(const f16x8*)(A + abase[i] + kk);
+        ra[i] = v;
       }
-      ra[i] = v;
+    } else {
+      int dy, dx;
+      if (p.kw == 3) {
+        dy = (tap * 11) >> 5;  // tap / 3 for tap < 9
+        dx = tap - 3 * dy;
+      } else {
+        dy = tap / p.kw;
+        dx = tap - dy * p.kw;
+      }
+      const long coff = (long)cv * 8;
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        f16x8 v = {};
+        int hi = ahb[i] + dy, wi = awb[i] + dx;
+        if (arow_ok[i] && kok && hi >= 0 && hi < Hl && wi >= 0 && wi < Wl) {
+          hi >>= p.up;
+          wi >>= p.up;
+          v = *(const f16x8*)(A + abase[i] + ((long)hi * p.IW + wi) * p.Cin + coff);
+        }
+        ra[i] = v;
+      }
+    }
+  };
+  auto advance = [&]() {
+    if (MODE == 1) {
+      cv += 8;
+      while (cv >= p.cin_vecs) {
+        cv -= p.cin_vecs;
+        ++tap;
+      }
     }
   };
   auto loadB = [&](int k0, f16x8 (&rb)[BV]) {
+    const int kk = k0 + chunk * 8;
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      int n = n0 + (tid >> 2) + 64 * i;
+      const int n = n0 + rbase + 32 * i;
       f16x8 v = {};
-      if (n < p.N && k0 + chunk * 8 < p.Kvalid) v = *(const f16x8*)(Wt + (long)n * p.ldw + k0 + chunk * 8);
+      if (n < p.N && kk < p.Kvalid) v = *(const f16x8*)(Wt + (long)n * p.ldw + kk);
       rb[i] = v;
     }
   };
   auto store = [&](int buf, const f16x8 (&ra)[AV], const f16x8 (&rb)[BV]) {
     f16* la = lds[buf];
-    f16* lb = lds[buf] + BM * LDSK;
+    f16* lb = lds[buf] + BM * BK;
 #pragma unroll
-    for (int i = 0; i < AV; ++i) *(f16x8*)(la + ((tid >> 2) + 64 * i) * LDSK + chunk * 8) = ra[i];
+    for (int i = 0; i < AV; ++i) {
+      const int row = rbase + 32 * i;
+      *(f16x8*)(la + row * BK + ((chunk ^ (row & 7)) << 3)) = ra[i];
+    }
 #pragma unroll
-    for (int i = 0; i < BV; ++i) *(f16x8*)(lb + ((tid >> 2) + 64 * i) * LDSK + chunk * 8) = rb[i];
+    for (int i = 0; i < BV; ++i) {
+      const int row = rbase + 32 * i;
+      *(f16x8*)(lb + row * BK + ((chunk ^ (row & 7)) << 3)) = rb[i];
+    }
   };
 
   f32x4 acc[RM][RN];
@@ -122,31 +165,43 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmP p) {
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   f16x8 ra[AV], rb[BV];
-  const int nk = p.K / BK;
+  const int nk = (p.K + BK - 1) / BK;
   loadA(0, ra);
   loadB(0, rb);
+  advance();
   store(0, ra, rb);
   __syncthreads();
   int cur = 0;
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
       loadA((kt + 1) * BK, ra);
       loadB((kt + 1) * BK, rb);
+      advance();
     }
-    const f16* la = lds[cur] + (wm * WTM) * LDSK;
-    const f16* lb = lds[cur] + BM * LDSK + (wn * WTN) * LDSK;
-    f16x8 af[RM], bf[RN];
+    const f16* la = lds[cur] + (wm * WTM) * BK;
+    const f16* lb = lds[cur] + BM * BK + (wn * WTN) * BK;
 #pragma unroll
-    for (int i = 0; i < RM; ++i) af[i] = *(const f16x8*)(la + (i * 16 + fr) * LDSK + fk);
+    for (int s = 0; s < 2; ++s) {
+      const int lc = 4 * s + fq;
+      f16x8 af[RM], bf[RN];
 #pragma unroll
-    for (int j = 0; j < RN; ++j) bf[j] = *(const f16x8*)(lb + (j * 16 + fr) * LDSK + fk);
+      for (int i = 0; i < RM; ++i) {
+        const int row = i * 16 + fr;  // (wm*WTM) is a multiple of 8: same swizzle phase
+        af[i] = *(const f16x8*)(la + row * BK + ((lc ^ (row & 7)) << 3));
+      }
 #pragma unroll
-    for (int i = 0; i < RM; ++i)
+      for (int j = 0; j < RN; ++j) {
+        const int row = j * 16 + fr;
+        bf[j] = *(const f16x8*)(lb + row * BK + ((lc ^ (row & 7)) << 3));
+      }
 #pragma unroll
-      for (int j = 0; j < RN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
     if (more) store(cur ^ 1, ra, rb);
     __syncthreads();
     cur ^= 1;
@@ -160,7 +215,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmP p) {
     for (int i = 0; i < RM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
         if (m >= p.M) continue;
         const float* rbrow = p.rowbias ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
 #pragma unroll
@@ -186,7 +241,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmP p) {
     for (int i = 0; i < RM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
         if (m >= p.M) continue;
 #pragma unroll
         for (int j = 0; j < RN / 2; ++j) {
@@ -207,14 +262,22 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmP p) {
   }
 }
 
-int launch(const GemmP& p, int batch, hipStream_t s, bool force128) {
-  if (force128 || p.N % 128 == 0) {
+template <int MODE>
+void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
+  if (force128 || p.N % 128 == 0 || p.N > 512) {
     dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
-    hipLaunchKernelGGL((gemm_kernel<128, 128>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<128, 128, MODE>), g, dim3(256), 0, s, p);
   } else {
     dim3 g(rdmi::div_up(p.N, 64), rdmi::div_up(p.M, 256), batch);
-    hipLaunchKernelGGL((gemm_kernel<256, 64>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<256, 64, MODE>), g, dim3(256), 0, s, p);
   }
+}
+
+int launch(const GemmP& p, int batch, hipStream_t s, bool force128, bool conv) {
+  if (conv)
+    launch_mode<1>(p, batch, s, force128);
+  else
+    launch_mode<0>(p, batch, s, force128);
   return rdmi::check_launch("gemm");
 }
 
@@ -237,10 +300,10 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.bias = a->bias; p.R = (const f16*)a->residual; p.ldr = a->ldr; p.sR = a->strideR;
   p.rowbias = a->rowbias; p.rpg = a->rows_per_group > 0 ? a->rows_per_group : 1; p.rb_ld = a->rowbias_ld;
   p.alpha = a->alpha;
-  p.M = a->M; p.N = a->N; p.K = (a->K + 31) / 32 * 32; p.Kvalid = a->K;
+  p.M = a->M; p.N = a->N; p.K = (a->K + BK - 1) / BK * BK; p.Kvalid = a->K;
   p.geglu = a->epilogue == RDMI_EPI_GEGLU;
   p.silu = a->epilogue == RDMI_EPI_SILU;
-  return launch(p, a->batch, (hipStream_t)stream, p.geglu);
+  return launch(p, a->batch, (hipStream_t)stream, p.geglu, false);
 }
 
 extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
@@ -248,7 +311,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   RDMI_REQUIRE(a->Cin % 8 == 0, RDMI_E_ALIGN, "conv2d: Cin (%d) must be a multiple of 8", a->Cin);
   RDMI_REQUIRE(a->B > 0 && a->H > 0 && a->W > 0 && a->Cout > 0 && a->Ho > 0 && a->Wo > 0, RDMI_E_ARG, "conv2d: bad sizes");
   const int K = a->kh * a->kw * a->Cin;
-  RDMI_REQUIRE(a->Kp >= K && a->Kp % 32 == 0, RDMI_E_ARG, "conv2d: Kp (%d) must be >= %d and a multiple of 32", a->Kp, K);
+  RDMI_REQUIRE(a->Kp >= K && a->Kp % 8 == 0, RDMI_E_ARG, "conv2d: Kp (%d) must be >= %d and a multiple of 8", a->Kp, K);
   RDMI_REQUIRE(al16(a->x) && al16(a->w), RDMI_E_ALIGN, "conv2d: x/w not 16-byte aligned");
   GemmP p{};
   p.A = (const f16*)a->x; p.Wt = (const f16*)a->w; p.ldw = a->Kp;
@@ -257,8 +320,12 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   p.rowbias = a->rowbias; p.rpg = a->Ho * a->Wo; p.rb_ld = a->rowbias_ld;
   p.alpha = a->alpha;
   p.M = a->B * a->Ho * a->Wo; p.N = a->Cout; p.K = a->Kp; p.Kvalid = K;
-  p.conv = 1; p.IH = a->H; p.IW = a->W; p.Cin = a->Cin; p.Ho = a->Ho; p.Wo = a->Wo;
+  p.IH = a->H; p.IW = a->W; p.Cin = a->Cin; p.Ho = a->Ho; p.Wo = a->Wo;
   p.kh = a->kh; p.kw = a->kw; p.stride = a->stride; p.pt = a->pad_top; p.pl = a->pad_left;
   p.up = a->upsample ? 1 : 0; p.cin_vecs = a->Cin / 8;
-  return launch(p, 1, (hipStream_t)stream, false);
+  // a 1×1, stride-1, unpadded conv on NHWC is a dense GEMM over pixels (conv_shortcut, quant convs)
+  const bool dense = a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad_top == 0 && a->pad_left == 0 && !a->upsample &&
+                     a->Ho == a->H && a->Wo == a->W;
+  if (dense) p.lda = a->Cin;
+  return launch(p, 1, (hipStream_t)stream, false, !dense);
 }

@@ -96,28 +96,53 @@ __global__ void gn_finalize(const double* __restrict__ part, int B, int G, int s
   mean_rstd[2 * i + 1] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// Streaming apply: each thread owns one 8-channel column (its 16 scale/shift values stay in
+// registers) and walks rows; no per-element division, 16-B loads/stores.
 __global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* __restrict__ y, long HW, int C,
-                                                int G, long nvec, const float* __restrict__ mr,
+                                                int G, int rows_per_block, const float* __restrict__ mr,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 int silu) {
   const int CV = C >> 3;
   const int cpg = C / G;
-  for (long v = blockIdx.x * (long)blockDim.x + threadIdx.x; v < nvec; v += (long)gridDim.x * blockDim.x) {
-    long pix = v / CV;
-    int c0 = (int)(v - pix * CV) * 8;
-    int b = (int)(pix / HW);
-    f16x8 in = *(const f16x8*)(x + v * 8);
-    f16x8 out;
+  const int b = blockIdx.y;
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = r0 + rows_per_block < HW ? r0 + rows_per_block : HW;
+  const int T = blockDim.x;
+  const int RL = CV >= T ? 1 : T / CV;
+  const int t = threadIdx.x;
+  const f16* xb = x + (long)b * HW * C;
+  f16* yb = y + (long)b * HW * C;
+  for (int cv0 = 0; cv0 < CV; cv0 += (CV >= T ? T : CV)) {
+    int cv, rl;
+    if (CV >= T) {
+      cv = cv0 + t;
+      rl = 0;
+      if (cv >= CV) break;
+    } else {
+      cv = t % CV;
+      rl = t / CV;
+      if (rl >= RL) break;
+    }
+    float sc[8], sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      int c = c0 + e;
+      int c = cv * 8 + e;
       int g = c / cpg;
       float mean = mr[2 * (b * G + g)], rstd = mr[2 * (b * G + g) + 1];
-      float f = ((float)in[e] - mean) * rstd * gamma[c] + beta[c];
-      if (silu) f = silu_f(f);
-      out[e] = (f16)f;
+      sc[e] = rstd * gamma[c];
+      sh[e] = beta[c] - mean * sc[e];
     }
-    *(f16x8*)(y + v * 8) = out;
+    for (long r = r0 + rl; r < r1; r += RL) {
+      f16x8 in = *(const f16x8*)(xb + r * C + cv * 8);
+      f16x8 out;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float f = fmaf((float)in[e], sc[e], sh[e]);
+        if (silu) f = silu_f(f);
+        out[e] = (f16)f;
+      }
+      *(f16x8*)(yb + r * C + cv * 8) = out;
+    }
   }
 }
 
@@ -204,11 +229,16 @@ extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int 
                                     const float* gamma, const float* beta, int silu, void* stream) {
   RDMI_REQUIRE(x && y && mean_rstd && gamma && beta, RDMI_E_ARG, "groupnorm_apply: null pointer");
   RDMI_REQUIRE(C % 8 == 0 && C % G == 0, RDMI_E_ARG, "groupnorm_apply: bad C=%d G=%d", C, G);
-  long nvec = (long)B * HW * C / 8;
-  long grid = (nvec + 255) / 256;
-  if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(gn_apply, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, HW,
-                     C, G, nvec, mean_rstd, gamma, beta, silu);
+  const int CV = C / 8;
+  const int T = CV >= 256 ? 256 : (256 / CV) * CV;
+  const int RL = CV >= T ? 1 : T / CV;
+  // ~2048 workgroups over the whole tensor, at least RL rows (one pass of the row lanes) each
+  long rpb = ((long)HW * B + 2047) / 2048;
+  if (rpb < RL) rpb = RL;
+  rpb = (rpb + RL - 1) / RL * RL;
+  dim3 g((unsigned)((HW + rpb - 1) / rpb), B);
+  hipLaunchKernelGGL(gn_apply, g, dim3(T), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
+                     mean_rstd, gamma, beta, silu);
   return rdmi::check_launch("groupnorm_apply");
 }
 

@@ -1,0 +1,107 @@
+"""Kernel micro-benchmarks at the metric configuration's shapes (768², snippet batch 8, VAE batch 8).
+
+    python tools/kbench.py [--only conv,gemm,attn,gn] [--iters 20]
+
+Prints achieved TFLOP/s (MFMA kernels) or GB/s (streaming kernels) per shape, timed with HIP
+events on the launch stream, random data (zeros inflate clocks, guide §5.4 rule 25)."""
+import argparse
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rollingdepth_amd import kernels as K  # noqa: E402
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def conv_cases():
+    # (label, B, H, W, Cin, Cout, up)
+    return [
+        ("unet L0 320->320 96^2 x24", 24, 96, 96, 320, 320, False),
+        ("unet L1 640->640 48^2 x24", 24, 48, 48, 640, 640, False),
+        ("unet L2 1280->1280 24^2 x24", 24, 24, 24, 1280, 1280, False),
+        ("unet L3 1280->1280 12^2 x24", 24, 12, 12, 1280, 1280, False),
+        ("unet up 960->320 96^2 x24", 24, 96, 96, 960, 320, False),
+        ("vae 512->512 96^2 x8", 8, 96, 96, 512, 512, False),
+        ("vae 512->512 192^2 x8", 8, 192, 192, 512, 512, False),
+        ("vae 256->256 384^2 x8", 8, 384, 384, 256, 256, False),
+        ("vae 128->128 768^2 x8", 8, 768, 768, 128, 128, False),
+        ("vae up 256 192->384 x8", 8, 192, 192, 256, 256, True),
+    ]
+
+
+def bench_conv(iters):
+    for lab, B, H, W, ci, co, up in conv_cases():
+        x = torch.randn(B, H, W, ci, device="cuda").half()
+        w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
+        Ho, Wo = (2 * H, 2 * W) if up else (H, W)
+        out = torch.empty(B, Ho, Wo, co, device="cuda", dtype=torch.float16)
+        ms = timeit(lambda: K.conv2d(x, w, co, 3, upsample=up, out=out), iters)
+        fl = 2.0 * B * Ho * Wo * co * ci * 9
+        print(f"conv  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
+
+
+def bench_gemm(iters):
+    for lab, M, N, Kd, geglu in [("L0 qkv 221k x 960 x 320", 221184, 960, 320, False),
+                                 ("L0 ff1 geglu 221k x 2560 x 320", 221184, 2560, 320, True),
+                                 ("L0 ff2 221k x 320 x 1280", 221184, 320, 1280, False),
+                                 ("L2 ff1 geglu 13.8k x 10240 x 1280", 13824, 10240, 1280, True),
+                                 ("L2 ff2 13.8k x 1280 x 5120", 13824, 1280, 5120, False)]:
+        a = torch.randn(M, Kd, device="cuda").half()
+        w = K.pack_linear(torch.randn(N, Kd) / math.sqrt(Kd), "cuda")
+        ms = timeit(lambda: K.gemm(a, w, Kd, geglu=geglu), iters)
+        fl = 2.0 * M * N * Kd
+        print(f"gemm  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
+
+
+def bench_attn(iters):
+    for lab, B, S, H in [("L0 S=27648 H=5 b=8", 8, 27648, 5), ("L1 S=6912 H=10 b=8", 8, 6912, 10),
+                         ("L2 S=1728 H=20 b=8", 8, 1728, 20), ("mid S=432 H=20 b=8", 8, 432, 20)]:
+        C = H * 64
+        qkv = torch.randn(B, S, 3 * C, device="cuda").half()
+        q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        out = torch.empty(B, S, C, device="cuda", dtype=torch.float16)
+        ms = timeit(lambda: K.attention(q, k, v, H, out=out), max(2, iters // 4))
+        fl = 4.0 * B * H * S * S * 64
+        print(f"attn  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
+
+
+def bench_gn(iters):
+    for lab, B, HW, C in [("unet 320 96^2 x24", 24, 9216, 320), ("vae 128 768^2 x8", 8, 589824, 128),
+                          ("vae 256 384^2 x8", 8, 147456, 256)]:
+        x = torch.randn(B, HW, C, device="cuda").half()
+        g = torch.ones(C, device="cuda")
+        b = torch.zeros(C, device="cuda")
+        out = torch.empty_like(x)
+        ms_s = timeit(lambda: K.groupnorm_stats(x, 32, 1e-5), iters)
+        mr = K.groupnorm_stats(x, 32, 1e-5)
+        from rollingdepth_amd._native import lib
+        ms_a = timeit(lambda: lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), B, HW, C, 32, mr.data_ptr(),
+                                                       g.data_ptr(), b.data_ptr(), 1, K._stream()), iters)
+        by = x.numel() * 2
+        print(f"gn    {lab:32s} stats {ms_s * 1e3:8.1f} us {by / ms_s / 1e6:7.0f} GB/s | apply {ms_a * 1e3:8.1f} us "
+              f"{2 * by / ms_a / 1e6:7.0f} GB/s")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="conv,gemm,attn,gn")
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    for part in a.only.split(","):
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn}[part](a.iters)
