@@ -52,6 +52,27 @@ def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) ->
     return out[:total]
 
 
+def local_rows(snippets: Sequence[torch.Tensor], counts: Sequence[int], world: int, rank: int) -> torch.Tensor:
+    """This rank's decoded snippets in flat (dilation, snippet) order → [rows, w, H, W]."""
+    flat = flat_snippets(counts)
+    lo, hi = chunk_bounds(len(flat), world)[rank]
+    ref = next(s for s in snippets if s is not None)
+    out = torch.empty((max(hi - lo, 0), *ref.shape[1:]), dtype=ref.dtype, device=ref.device)
+    for i, (d, k) in enumerate(flat[lo:hi]):
+        out[i] = snippets[d][k]
+    return out
+
+
+def gather_snippets(local: torch.Tensor, counts: Sequence[int], world: int, group=None) -> List[torch.Tensor]:
+    """All-gather every rank's rows and split them back per dilation."""
+    allsn = _all_gather_rows(local, sum(counts), world, group)
+    per_d, o = [], 0
+    for n in counts:
+        per_d.append(allsn[o:o + n])
+        o += n
+    return per_d
+
+
 @torch.no_grad()
 def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool = True,
                     snippet_len: int = 3, coalign_kwargs=None, init_noise: torch.Tensor = None, group=None):
@@ -87,19 +108,11 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     subsets = rank_subsets(counts, world, rank)
     snippets = pipe.init_snippet_infer(rgb_latent, noise, dil, [snippet_len] * len(dil), [1] * len(dil),
                                        [1] * len(dil), snippet_subset=subsets)
-    flat = flat_snippets(counts)
-    slo, shi = chunk_bounds(len(flat), world)[rank]
-    local = torch.empty((max(shi - slo, 0), snippet_len, H, W), dtype=F16, device=dev)
-    for i, (d, k) in enumerate(flat[slo:shi]):
-        local[i] = snippets[d][k]  # my rows, in flat order
+    local = local_rows(snippets, counts, world, rank)
     # 3. all-gather decoded snippets, co-align on rank 0
-    allsn = _all_gather_rows(local, len(flat), world, group)
+    per_d = gather_snippets(local, counts, world, group)
     if rank != 0:
         return None, None
-    per_d, o = [], 0
-    for n in counts:
-        per_d.append(allsn[o:o + n])
-        o += n
     aligner = DepthAligner(device=dev, **(coalign_kwargs or {}))
     merged, _, _, _ = aligner.run([s.view(s.shape[0], snippet_len, 1, H, W) for s in per_d], dil)
     d = merged.float().contiguous()

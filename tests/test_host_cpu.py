@@ -1,0 +1,107 @@
+"""CPU tests of the host side: librdmi loads and exports every entry point include/rdmi.h declares
+(no compute calls without a GPU), weight packing layouts, snippet scheduling, DDIM coefficients,
+sharding partition logic."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import rd_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    from rollingdepth_amd import _native
+
+    hdr = open(os.path.join(ROOT, "include", "rdmi.h")).read()
+    declared = set(re.findall(r"\b(rdmi_[a-z0-9_]+)\s*\(", hdr))
+    assert declared, "no declarations parsed"
+    for name in declared:
+        assert hasattr(_native.lib, name), f"librdmi.so does not export {name}"
+    assert declared == set(_native.EXPORTED), declared ^ set(_native.EXPORTED)
+    assert _native.lib.rdmi_version() >= 1
+
+
+def test_error_reporting_without_gpu():
+    """Argument validation runs before any launch, so bad calls fail loudly on the host."""
+    import ctypes as C
+    from rollingdepth_amd import _native
+
+    g = _native.GemmArgs()
+    rc = _native.lib.rdmi_gemm(C.byref(g), None)
+    assert rc == 1001
+    assert b"null" in _native.lib.rdmi_last_error()
+    with pytest.raises(_native.RdmiError):
+        _native.check(rc, "rdmi_gemm")
+
+
+def test_pack_conv_layout():
+    from rollingdepth_amd import kernels as K
+
+    w = torch.randn(5, 3, 3, 3)
+    p = K.pack_conv(w, "cpu", 8)
+    assert p.shape == (5, 96)
+    t = p[:, :72].float().view(5, 3, 3, 8)
+    assert torch.allclose(t[..., :3], w.permute(0, 2, 3, 1).half().float())
+    assert t[..., 3:].abs().max() == 0 and p[:, 72:].abs().max() == 0
+
+
+def test_geglu_permutation_roundtrip():
+    from rollingdepth_amd import kernels as K
+
+    w = torch.arange(256 * 2).float().view(256, 2)
+    b = torch.arange(256).float()
+    wp, bp = K.geglu_permute(w, b)
+    # slab s: value rows 32s..32s+31 then gate rows 128+32s..
+    assert torch.equal(bp[:32], b[:32]) and torch.equal(bp[32:64], b[128:160])
+    assert sorted(bp.tolist()) == b.tolist()
+
+
+def test_snippet_scheduling_matches_golden():
+    import json
+    from rollingdepth_amd.pipeline import RollingDepthPipeline as P
+
+    idx = json.load(open(os.path.join(ROOT, "tests", "golden", "snippet_indices.json")))
+    for n, w, d, capped in idx["cap"]:
+        assert P.cap_max_dilation(n, w, d) == capped
+    for n, spec, expect in idx["snippets"]:
+        if isinstance(spec, list):
+            ds, de, i_step, T = spec
+            assert P.get_snippet_indice(i_step, list(range(T)), n, 3, ds, de, 1) == expect
+        else:
+            assert P.get_snippet_indice(0, [999], n, 3, spec, spec, 1) == expect
+
+
+def test_ddim_coefficients_vs_oracle():
+    from rollingdepth_amd.config import RD_SCHEDULER
+    from rollingdepth_amd.scheduler import DDIMScheduler
+
+    s = DDIMScheduler.from_config(RD_SCHEDULER)
+    o = O.DDIM(RD_SCHEDULER)
+    x, e = torch.randn(1000), torch.randn(1000)
+    for n in (1, 10):
+        s.set_timesteps(n)
+        ts = o.set_timesteps(n)
+        assert s.timesteps.tolist() == ts
+        for t in ts:
+            ca, cb = s.step_coefficients(t)
+            torch.testing.assert_close(ca * x + cb * e, o.step(e, t, x), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("counts,world", [([98, 50], 1), ([98, 50], 2), ([98, 50], 8), ([498, 480, 450], 8),
+                                          ([7, 5], 4), ([3], 8)])
+def test_shard_partition_covers_every_snippet_once(counts, world):
+    from rollingdepth_amd.shard import chunk_bounds, flat_snippets, rank_subsets
+
+    seen = []
+    for r in range(world):
+        sub = rank_subsets(counts, world, r)
+        for d, ks in enumerate(sub):
+            assert ks == sorted(ks) and (not ks or ks == list(range(ks[0], ks[-1] + 1)))
+            seen += [(d, k) for k in ks]
+    assert seen == flat_snippets(counts)
+    sizes = [hi - lo for lo, hi in chunk_bounds(sum(counts), world)]
+    assert max(sizes) - min(s for s in sizes if s) <= max(1, max(sizes))

@@ -67,3 +67,30 @@ def test_snippet_batching_invariance():
     b = _run("tiny_pipeline", snippet_batch=1)
     for x, y in zip(a[2].snippet_ls, b[2].snippet_ls):
         assert torch.equal(x, y)
+
+
+def test_sharded_forward_world1_equals_forward():
+    """shard.sharded_forward over a 1-rank RCCL group reproduces pipe.forward bitwise."""
+    import socket
+    import torch.distributed as dist
+    from rollingdepth_amd.shard import sharded_forward
+
+    t, meta, out, rec, dil = _run("tiny_pipeline")
+    from rollingdepth_amd.pipeline import RollingDepthPipeline
+
+    pipe = RollingDepthPipeline.from_synthetic(meta["unet"], meta["vae"], meta["scheduler"], device="cuda")
+    pipe.empty_text_embed = t["context"]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        depth, per_d = sharded_forward(pipe, t["frames"][None].cuda(), list(meta["dilations_in"]), True, 3, None,
+                                       init_noise=t["init_noise"].cuda())
+    finally:
+        dist.destroy_process_group()
+    for a, b in zip(per_d, out.snippet_ls):
+        assert torch.equal(a.cpu(), b.view(a.shape))
+    assert torch.equal(depth.cpu(), out.depth_pred)
