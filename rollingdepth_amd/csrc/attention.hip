@@ -1,13 +1,15 @@
 // Cross-frame attention kernels.
 //
 // attn_fwd_d64: flash-style fused softmax(q kᵀ·scale) v for head_dim 64 on gfx950.
-//   Workgroup = 4 waves × 32 queries (128 queries) of one (batch, head); 64-key K/V tiles are
-//   staged through LDS (register-staged double buffer; K XOR-swizzled per 16-B chunk).
+//   Workgroup = 8 waves × 32 queries (256 queries) of one (batch, head); 64-key K/V tiles arrive
+//   by LDS-DMA into a 3-slot ring (two tiles in flight; K XOR-swizzled per 16-B chunk through the
+//   source address).
 //   Per wave and tile: Sᵀ = K·Qᵀ with v_mfma_f32_32x32x16_f16 (Q fragments live in registers for
 //   the whole sweep), so each lane owns one query's scores ("swapped QKᵀ": the row max/sum is
 //   lane-local plus one lane^32 exchange); Oᵀ = Vᵀ·Pᵀ with the P accumulator re-used directly
 //   as the B operand (keys in the MFMA's permuted k order) and V read from LDS with
-//   ds_read_b64_tr_b16 (hardware transpose).  Online softmax in exp2 domain, f32 throughout.
+//   ds_read_b64_tr_b16 (hardware transpose).  Online softmax in exp2 domain, f32 throughout; the
+//   O rescale is skipped (exactly) on tiles where no lane's running max moved.
 // attn_smallkv: attention of every query token against ≤ 16 shared keys (the UNet's
 //   cross-attention to the 2-token empty-text context) — a streaming kernel, no MFMA.
 // softmax_rows: f32 scores → f16 probabilities, for the d=C single-head VAE attention that is
@@ -23,12 +25,24 @@ struct AttnP {
   float sl2;  // scale * log2(e)
 };
 
-constexpr int QB = 128;  // queries per workgroup
-constexpr int KB = 64;   // keys per tile
+constexpr int NWV = 8;        // waves per workgroup
+constexpr int QB = 32 * NWV;  // queries per workgroup (32 per wave)
+constexpr int KB = 64;        // keys per tile
+constexpr int TILE = KB * 64; // halves per K (or V) tile
 
-__global__ __launch_bounds__(256, 2) void attn_fwd_d64(AttnP p) {
-  __shared__ __attribute__((aligned(16))) f16 Ks[2][KB * 64];
-  __shared__ __attribute__((aligned(16))) f16 Vs[2][KB * 64];
+__device__ f16x8 g_attn_zero16;
+
+template <int N>
+__device__ __forceinline__ void attn_wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4) into a 3-slot ring (no VGPR staging,
+// no ds_write): each wave moves 8 key rows of K and of V per tile.  K's 16-B chunks are
+// XOR-swizzled by (key & 7) through the per-lane source address; V stays row-major for the
+// transposed reads.
+__global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
+  __shared__ __attribute__((aligned(16))) f16 lds[3 * 2 * TILE];  // 48 KB: slot s = [K | V]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -50,33 +64,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_d64(AttnP p) {
     qf[ks] = qi < p.Sq ? *(const f16x8*)(Q + (long)qi * p.q_ld + ks * 16 + hh * 8) : z;
   }
 
-  // staging: 512 16-B vectors per tile per tensor; thread → vectors tid, tid+256
-  f16x8 rk[2], rv[2];
-  auto load_tile = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int vi = tid + 256 * i;
-      int key = kt * KB + (vi >> 3);
-      int ch = vi & 7;
-      f16x8 z = {};
-      if (key < p.Sk) {
-        rk[i] = *(const f16x8*)(K + (long)key * p.k_ld + ch * 8);
-        rv[i] = *(const f16x8*)(V + (long)key * p.v_ld + ch * 8);
-      } else {
-        rk[i] = z;
-        rv[i] = z;
-      }
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int vi = tid + 256 * i;
-      int key = vi >> 3;
-      int ch = vi & 7;
-      *(f16x8*)(&Ks[buf][key * 64 + ((ch ^ (key & 7)) << 3)]) = rk[i];
-      *(f16x8*)(&Vs[buf][key * 64 + ch * 8]) = rv[i];
-    }
+  // DMA lane geometry: 8 rows x 8 chunks per 1-KiB instruction
+  const int drow = lane >> 3;
+  const int kchunk = (lane & 7) ^ drow;  // K: logical chunk stored at phys (lane & 7)
+  const int vchunk = lane & 7;
+  const f16* zero = (const f16*)&g_attn_zero16;
+  auto issue = [&](int kt, int slot) {
+    const int key = kt * KB + wid * 8 + drow;
+    const bool ok = key < p.Sk;
+    f16* ks_ = lds + slot * 2 * TILE + wid * 8 * 64;
+    __builtin_amdgcn_global_load_lds(ok ? (const void*)(K + (long)key * p.k_ld + kchunk * 8) : (const void*)zero,
+                                     (__attribute__((address_space(3))) void*)ks_, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(ok ? (const void*)(V + (long)key * p.v_ld + vchunk * 8) : (const void*)zero,
+                                     (__attribute__((address_space(3))) void*)(ks_ + TILE), 16, 0, 0);
   };
 
   f32x16 o[2];
@@ -87,20 +87,21 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_d64(AttnP p) {
   float m = -INFINITY, l = 0.f;
 
   const int nt = (p.Sk + KB - 1) / KB;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  int cur = 0;
   // tr-read lane geometry (16-lane groups)
   const int gi = lane >> 4, li = lane & 15;
   const int tr_key = 4 * (gi >> 1) + (li >> 2);
   const int tr_col = 16 * (gi & 1) + 4 * (li & 3);
+  issue(0, 0);
+  issue(1, 1);  // zero rows when nt == 1: keeps exactly 2 younger DMAs in flight at every wait
 
   for (int kt = 0; kt < nt; ++kt) {
-    const bool more = kt + 1 < nt;
-    if (more) load_tile(kt + 1);
-    const f16* ks_ = Ks[cur];
-    const f16* vs_ = Vs[cur];
+    attn_wait_vmcnt<2>();  // this wave's DMAs of tile kt landed (tile kt+1 in flight)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of kt landed; every wave done with kt-1
+    asm volatile("" ::: "memory");
+    issue(kt + 2, (kt + 2) % 3);   // past the end: zero rows into the drained slot
+    const f16* ks_ = lds + (kt % 3) * 2 * TILE;
+    const f16* vs_ = ks_ + TILE;
     // ---- Sᵀ = K · Qᵀ for 2 key blocks of 32
     f32x16 s[2];
 #pragma unroll
@@ -118,19 +119,34 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_d64(AttnP p) {
     // ---- mask + online softmax (lane owns query c, keys (r&3)+8(r>>2)+4hh of each block)
     const int kbase = kt * KB;
     float mx = -INFINITY;
+    if (kbase + KB <= p.Sk) {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (key >= p.Sk) s[kb][r] = -INFINITY;
-        mx = fmaxf(mx, s[kb][r]);
-      }
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key >= p.Sk) s[kb][r] = -INFINITY;
+          mx = fmaxf(mx, s[kb][r]);
+        }
+    }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f((m - mn) * p.sl2);
-    const float msc = mn * p.sl2;
-    m = mn;
+    // exact T13: rescale O only when some lane's running max moved (alpha == 1 otherwise)
+    if (__any(mn > m)) {
+      const float alpha = exp2f((m - mn) * p.sl2);
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      m = mn;
+    }
+    const float msc = m * p.sl2;
     float rs = 0.f;
     f16x8 pf[4];
 #pragma unroll
@@ -141,11 +157,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_d64(AttnP p) {
         rs += e;
         pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
       }
-    l = l * alpha + rs;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    l += rs;
     // ---- Oᵀ += Vᵀ · Pᵀ (4 k-steps of 16 keys, 2 d-blocks of 32)
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
@@ -161,10 +173,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_d64(AttnP p) {
         o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[st], o[d], 0, 0, 0);
       }
     }
-    if (more) store_tile(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
   }
+  attn_wait_vmcnt<0>();  // drain trailing zero-row DMAs before the workgroup retires
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = 1.f / lt;
   if (qi < p.Sq) {
@@ -278,7 +288,7 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
   AttnP p{(const f16*)q, (const f16*)k, (const f16*)v, (f16*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs,
           scale * 1.4426950408889634f};
   dim3 g(rdmi::div_up(Sq, QB), H, B);
-  hipLaunchKernelGGL(attn_fwd_d64, g, dim3(256), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(attn_fwd_d64, g, dim3(64 * NWV), 0, (hipStream_t)stream, p);
   return rdmi::check_launch("attention_fwd");
 }
 

@@ -28,21 +28,40 @@ struct GemmP {
   int IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
 };
 
+__device__ f16x8 g_zero16;  // source of the zero chunks (padding / out-of-range) for LDS-DMA
+
+__device__ __forceinline__ void glds16(const void* g, f16* l) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+// vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 // MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x (kh×kw conv).
-// LDS tiles are [rows][64] halves with the 16-B chunk index XOR-swizzled by (row & 7)
-// (conflict-spread ds_read_b128 fragment reads, cdna_hip_programming.md §5.5 T2).
-template <int BM, int BN, int MODE>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+// Operands reach LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no ds_write) into a
+// 3-slot ring of [rows][64-half] tiles, two K-steps in flight, one barrier per K-step.  Each
+// 1-KiB DMA instruction fills 8 rows lane-linearly; the 16-B chunk swizzle (phys = logical ^
+// (row & 7)) is applied on the per-lane SOURCE address and on the fragment read (guide rule 21),
+// so ds_read_b128 fragment reads are conflict-free.
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
+  constexpr int NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int AV = BM / 32;  // 16-B A vectors per thread per stage (8 chunks x BM rows / 256)
-  constexpr int BV = BN / 32;
-  __shared__ __attribute__((aligned(16))) f16 lds[2][(BM + BN) * BK];
+  constexpr int AV = BM / 8 / NW;  // 1-KiB DMA instructions per wave per stage (A)
+  constexpr int BV = BN / 8 / NW;
+  constexpr int LPS = AV + BV;     // DMA instructions per wave per stage
+  constexpr int SLOT = (BM + BN) * BK;
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile/waves mismatch");
+  __shared__ __attribute__((aligned(16))) f16 lds[3 * SLOT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   // XCD-aware remap (T1): dispatch id d runs on XCD d % 8; give each XCD a contiguous range of
   // logical tiles so the n-tiles sharing one A row-panel share that XCD's L2.
   const int nbx = gridDim.x, nby = gridDim.y;
@@ -59,14 +78,16 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
   const f16* A = p.A + (long)bz * p.sA;
   const f16* Wt = p.Wt + (long)bz * p.sW;
 
-  const int chunk = tid & 7;
-  const int rbase = tid >> 3;
+  // lane → (row within its 8-row DMA group, logical chunk): phys chunk = lane & 7
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ lrow;
+  // element offsets are 32-bit (every operand of this path is < 2^31 elements; checked on host)
   bool arow_ok[AV];
-  long abase[AV];
+  int abase[AV];
   int ahb[AV], awb[AV];
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
-    const int m = m0 + rbase + 32 * i;
+    const int m = m0 + (i * NW + wid) * 8 + lrow;
     arow_ok[i] = m < p.M;
     const int mm = arow_ok[i] ? m : 0;
     if (MODE == 1) {
@@ -77,29 +98,39 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
       const int wo = r - ho * p.Wo;
       ahb[i] = ho * p.stride - p.pt;
       awb[i] = wo * p.stride - p.pl;
-      abase[i] = (long)b * p.IH * p.IW * p.Cin;
+      abase[i] = b * p.IH * p.IW * p.Cin;
     } else {
-      abase[i] = (long)mm * p.lda;
+      abase[i] = mm * (int)p.lda;
       ahb[i] = awb[i] = 0;
     }
   }
-  // incremental (tap, channel-vector) of this thread's chunk: k-vector index = k0/8 + chunk
+  bool brow_ok[BV];
+  int bbase[BV];
+#pragma unroll
+  for (int i = 0; i < BV; ++i) {
+    const int n = n0 + (i * NW + wid) * 8 + lrow;
+    brow_ok[i] = n < p.N;
+    bbase[i] = (brow_ok[i] ? n : 0) * (int)p.ldw;
+  }
   int tap = 0, cv = chunk;
   if (MODE == 1) {
     tap = chunk / p.cin_vecs;
     cv = chunk - tap * p.cin_vecs;
   }
   const int Hl = p.IH << p.up, Wl = p.IW << p.up;
+  const f16* zero = (const f16*)&g_zero16;
 
-  auto loadA = [&](int k0, f16x8 (&ra)[AV]) {
-    const int kk = k0 + chunk * 8;
+  // issue the DMA of K-step `ks` into ring slot `slot`
+  auto issue = [&](int ks, int slot) {
+    const int kk = ks * BK + chunk * 8;
     const bool kok = kk < p.Kvalid;
+    f16* la = lds + slot * SLOT;
+    f16* lb = la + BM * BK;
     if (MODE == 0) {
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
-        f16x8 v = {};
-        if (arow_ok[i] && kok) v = *(const f16x8*)(A + abase[i] + kk);
-        ra[i] = v;
+        const bool ok = arow_ok[i] && kok;
+        glds16(ok ? A + (abase[i] + kk) : zero, la + (i * NW + wid) * 8 * BK);
       }
     } else {
       int dy, dx;
@@ -110,51 +141,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
         dy = tap / p.kw;
         dx = tap - dy * p.kw;
       }
-      const long coff = (long)cv * 8;
+      const int coff = cv * 8;
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
-        f16x8 v = {};
-        int hi = ahb[i] + dy, wi = awb[i] + dx;
-        if (arow_ok[i] && kok && hi >= 0 && hi < Hl && wi >= 0 && wi < Wl) {
-          hi >>= p.up;
-          wi >>= p.up;
-          v = *(const f16x8*)(A + abase[i] + ((long)hi * p.IW + wi) * p.Cin + coff);
-        }
-        ra[i] = v;
+        const int hi = ahb[i] + dy, wi = awb[i] + dx;
+        const bool ok = arow_ok[i] && kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
+        const int off = abase[i] + ((hi >> p.up) * p.IW + (wi >> p.up)) * p.Cin + coff;
+        glds16(ok ? A + off : zero, la + (i * NW + wid) * 8 * BK);
       }
-    }
-  };
-  auto advance = [&]() {
-    if (MODE == 1) {
       cv += 8;
       while (cv >= p.cin_vecs) {
         cv -= p.cin_vecs;
         ++tap;
       }
     }
-  };
-  auto loadB = [&](int k0, f16x8 (&rb)[BV]) {
-    const int kk = k0 + chunk * 8;
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      const int n = n0 + rbase + 32 * i;
-      f16x8 v = {};
-      if (n < p.N && kk < p.Kvalid) v = *(const f16x8*)(Wt + (long)n * p.ldw + kk);
-      rb[i] = v;
-    }
-  };
-  auto store = [&](int buf, const f16x8 (&ra)[AV], const f16x8 (&rb)[BV]) {
-    f16* la = lds[buf];
-    f16* lb = lds[buf] + BM * BK;
-#pragma unroll
-    for (int i = 0; i < AV; ++i) {
-      const int row = rbase + 32 * i;
-      *(f16x8*)(la + row * BK + ((chunk ^ (row & 7)) << 3)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      const int row = rbase + 32 * i;
-      *(f16x8*)(lb + row * BK + ((chunk ^ (row & 7)) << 3)) = rb[i];
+      const bool ok = brow_ok[i] && kok;
+      glds16(ok ? Wt + (bbase[i] + kk) : zero, lb + (i * NW + wid) * 8 * BK);
     }
   };
 
@@ -164,24 +168,19 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f16x8 ra[AV], rb[BV];
   const int nk = (p.K + BK - 1) / BK;
-  loadA(0, ra);
-  loadB(0, rb);
-  advance();
-  store(0, ra, rb);
-  __syncthreads();
-  int cur = 0;
+  issue(0, 0);
+  issue(1, 1);  // (a zero-chunk DMA when nk == 1: exactly LPS younger DMAs at every wait)
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) {
-      loadA((kt + 1) * BK, ra);
-      loadB((kt + 1) * BK, rb);
-      advance();
-    }
-    const f16* la = lds[cur] + (wm * WTM) * BK;
-    const f16* lb = lds[cur] + BM * BK + (wn * WTN) * BK;
+    wait_vmcnt<LPS>();  // this wave's DMA for step kt has landed (step kt+1 still in flight)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's DMA for kt landed; every wave done with kt-1
+    asm volatile("" ::: "memory");
+    // branch-free: past the last K-step the DMA reads the zero chunk into a drained slot
+    issue(kt + 2, (kt + 2) % 3);
+    const f16* la = lds + (kt % 3) * SLOT + (wm * WTM) * BK;
+    const f16* lb = lds + (kt % 3) * SLOT + BM * BK + (wn * WTN) * BK;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int lc = 4 * s + fq;
@@ -202,10 +201,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store(cur ^ 1, ra, rb);
-    __syncthreads();
-    cur ^= 1;
   }
+  wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
   const long cb = (long)bz * p.sC;
@@ -264,12 +261,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmP p) {
 
 template <int MODE>
 void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
+  const long mt256 = (p.M + 255) / 256;
   if (force128 || p.N % 128 == 0 || p.N > 512) {
-    dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
-    hipLaunchKernelGGL((gemm_kernel<128, 128, MODE>), g, dim3(256), 0, s, p);
+    if (mt256 * ((p.N + 127) / 128) * batch >= 512) {  // enough tiles to fill the chip with 256-row tiles
+      dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 256), batch);
+      hipLaunchKernelGGL((gemm_kernel<256, 128, 4, 2, MODE>), g, dim3(512), 0, s, p);
+    } else {
+      dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
+      hipLaunchKernelGGL((gemm_kernel<128, 128, 2, 2, MODE>), g, dim3(256), 0, s, p);
+    }
   } else {
     dim3 g(rdmi::div_up(p.N, 64), rdmi::div_up(p.M, 256), batch);
-    hipLaunchKernelGGL((gemm_kernel<256, 64, MODE>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_kernel<256, 64, 8, 1, MODE>), g, dim3(512), 0, s, p);
   }
 }
 
@@ -293,6 +296,8 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   RDMI_REQUIRE(al16(a->A) && al16(a->W) && a->strideA % 8 == 0 && a->strideW % 8 == 0, RDMI_E_ALIGN, "gemm: A/W not 16-byte aligned");
   RDMI_REQUIRE(a->epilogue != RDMI_EPI_GEGLU || a->N % 128 == 0, RDMI_E_ARG, "gemm: GEGLU needs N %% 128 == 0");
   RDMI_REQUIRE(!a->rowbias || a->rows_per_group > 0, RDMI_E_ARG, "gemm: rowbias needs rows_per_group");
+  RDMI_REQUIRE((long)a->M * a->lda < (1L << 31) && (long)a->N * a->ldw < (1L << 31), RDMI_E_ARG,
+               "gemm: operand exceeds 2^31 elements per batch");
   GemmP p{};
   p.A = (const f16*)a->A; p.lda = a->lda; p.sA = a->strideA;
   p.Wt = (const f16*)a->W; p.ldw = a->ldw; p.sW = a->strideW;
@@ -313,6 +318,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   const int K = a->kh * a->kw * a->Cin;
   RDMI_REQUIRE(a->Kp >= K && a->Kp % 8 == 0, RDMI_E_ARG, "conv2d: Kp (%d) must be >= %d and a multiple of 8", a->Kp, K);
   RDMI_REQUIRE(al16(a->x) && al16(a->w), RDMI_E_ALIGN, "conv2d: x/w not 16-byte aligned");
+  RDMI_REQUIRE((long)a->B * a->H * a->W * a->Cin < (1L << 31) && (long)a->Cout * a->Kp < (1L << 31), RDMI_E_ARG,
+               "conv2d: input exceeds 2^31 elements (split the batch)");
   GemmP p{};
   p.A = (const f16*)a->x; p.Wt = (const f16*)a->w; p.ldw = a->Kp;
   p.C = a->y; p.ldc = a->y_ld > 0 ? a->y_ld : a->Cout;
