@@ -120,9 +120,11 @@ int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, float scale
 /* ---------------------------------------------------------------------------------------
  * Layout / elementwise helpers (f16 NHWC unless stated)
  */
-/* NCHW (f32 if x_f32 else f16) → NHWC f16 with channel padding to Cpad (zeros), y = x*scale */
+/* NCHW (f32 if x_f32 else f16, batch/channel strides in elements; x_cstride = 0 replicates one
+ * channel, e.g. the depth → 3-channel repeat before re-encoding, rollingdepth_pipeline.py:327)
+ * → NHWC f16 with channel padding to Cpad (zeros), y = x*scale */
 int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int B, int C, int H, int W, int Cpad,
-                      float scale, void* stream);
+                      float scale, long x_bstride, long x_cstride, void* stream);
 /* NHWC f16 (ld = channel stride) → NCHW f32, first C channels, y = x*scale + shift */
 int rdmi_nhwc_to_nchw_f32(const void* x, long ld, float* y, int B, int C, int H, int W,
                           float scale, float shift, void* stream);
@@ -137,11 +139,17 @@ int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, 
 int rdmi_gather_unet_input(const void* rgb, long rgb_frame_ld, const void* depth,
                            long depth_frame_ld, int depth_bcast, const int* frame_idx, int count,
                            long HW, void* out, void* stream);
-/* DDIM step (eta = 0) as the affine map the 1-step scheduler reduces to
- * (scheduling_ddim.py:402-448): y = (ca·x + cb·e) * out_scale; x, e: [P] with strides, y [P, ld_y]
- * channels 0..C-1, channels C..Cpad-1 of y zeroed. */
+/* DDIM step (eta = 0) / add_noise as the affine map they reduce to (scheduling_ddim.py:402-448,
+ * :471-495): y = (ca·x + cb·e) * out_scale; x, e: [P] pixel rows with strides, y [P, ld_y]
+ * channels 0..C-1, channels C..Cpad-1 of y zeroed; e_period > 0 broadcasts e over pixel rows
+ * (the shared init noise of every frame, :282-288). */
 int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* y, long ld_y,
-                      long P, int C, int Cpad, float ca, float cb, float out_scale, void* stream);
+                      long P, int C, int Cpad, float ca, float cb, float out_scale, long e_period,
+                      void* stream);
+/* Refine averaging (rollingdepth_pipeline.py:586-629): out[f] = mean over the snippets s = f − j·stride
+ * (0 ≤ s < n) of src[s][j]; src [n][w][P][ld], out [N][P][ld] f16 (channels ≥ C zeroed). */
+int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld,
+                         void* out, void* stream);
 /* Global min/max of an f16 or f32 buffer → minmax[2] f32 (workspace ≥ 2*1024 floats)
  * (the `min([snippet.min() ...])` of depth_aligner.py:78 and the min/max of :316-317). */
 int rdmi_minmax(const void* x, int x_f32, long n, float* minmax, float* workspace, void* stream);

@@ -480,15 +480,41 @@ def snippet_denoise(usd, ucfg, sched: DDIM, rgb_lat, init_noise, idx_list, conte
     return torch.stack(outs)  # [n_d, w, 4, h, w]
 
 
+def refine(usd, ucfg, sched: DDIM, rgb_lat, depth_lat, init_noise, refine_step, snippet_len, start_dilation,
+           context, skip_t_ratio=0.5):
+    """RollingDepthPipeline.refine (rollingdepth_pipeline.py:517-633): add noise at the middle
+    timestep, then per step every snippet (gap shrinking start_dilation → 1) is denoised from the
+    OLD latents and each frame takes the mean of its snippets' predictions."""
+    N = rgb_lat.shape[0]
+    T = int(refine_step / skip_t_ratio)
+    ts = sched.set_timesteps(T)
+    ts = ts[int(len(ts) * skip_t_ratio):]
+    new = sched.add_noise(depth_lat, init_noise.expand_as(depth_lat), ts[0])
+    for i, t in enumerate(ts):
+        idx = snippet_indices(i, len(ts), N, snippet_len, start_dilation, 1)
+        old = new.clone()
+        acc = torch.zeros_like(new)
+        cnt = torch.zeros(N)
+        for ids in idx:
+            x = torch.cat([rgb_lat[ids], old[ids]], dim=1)
+            pred = unet_forward(usd, ucfg, x, torch.full((len(ids),), t, dtype=torch.long), context, len(ids))
+            acc[ids] += sched.step(pred, t, old[ids])
+            cnt[ids] += 1
+        new = acc / cnt[:, None, None, None]
+    return new
+
+
 def pipeline_forward(usd, ucfg, vsd, vcfg, scfg, frames: torch.Tensor, init_noise: torch.Tensor,
                      context: torch.Tensor, dilations: List[int], cap_dilation=True, snippet_len=3,
-                     coalign_kwargs=None, max_vae_bs=4, record=None):
-    """RollingDepthPipeline.forward (rollingdepth_pipeline.py:193-354), refine_step=0, stride 1.
+                     coalign_kwargs=None, max_vae_bs=4, record=None, refine_step=0, refine_snippet_len=3,
+                     refine_start_dilation=6):
+    """RollingDepthPipeline.forward (rollingdepth_pipeline.py:193-354), stride 1.
     frames [N,3,H,W] in [-1,1]; init_noise [1,4,h,w] (broadcast to all frames, :282-288)."""
     N = frames.shape[0]
     dil = list(dilations)
     if cap_dilation:
         dil = [cap_max_dilation(N, snippet_len, d) for d in dil]
+        refine_start_dilation = cap_max_dilation(N, refine_snippet_len, refine_start_dilation)
     rgb_lat = encode_frames(vsd, vcfg, frames, max_vae_bs)
     noise = init_noise.expand(N, *init_noise.shape[1:])
     sched = DDIM(scfg)
@@ -509,5 +535,12 @@ def pipeline_forward(usd, ucfg, vsd, vcfg, scfg, frames: torch.Tensor, init_nois
     d = d * 2.0 - 1.0
     if record is not None:
         record.update(rgb_latent=rgb_lat, snippets=snippets, scales=sc, translations=tr, hist=hist,
-                      dilations=dil)
+                      dilations=dil, depth_coaligned=d)
+    if refine_step > 0:
+        dlat = encode_frames(vsd, vcfg, d.expand(-1, 3, -1, -1), max_vae_bs)
+        new = refine(usd, ucfg, sched, rgb_lat, dlat, init_noise, refine_step, refine_snippet_len,
+                     refine_start_dilation, context)
+        if record is not None:
+            record.update(refined_latent=new)
+        d = decode_depth(vsd, vcfg, new, max_vae_bs)
     return d

@@ -12,14 +12,14 @@ inline unsigned grid_for(long n, int per_block = 256) {
 }
 
 __global__ void nchw_to_nhwc_k(const void* __restrict__ x, int x_f32, f16* __restrict__ y, int C, long HW, int Cpad,
-                               long n, float scale) {
+                               long n, float scale, long bstride, long cstride) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     long pix = i / Cpad;
     int c = (int)(i - pix * Cpad);
     long b = pix / HW, p = pix - b * HW;
     float v = 0.f;
     if (c < C) {
-      long src = (b * C + c) * HW + p;
+      long src = b * bstride + c * cstride + p;
       v = x_f32 ? ((const float*)x)[src] : (float)((const f16*)x)[src];
       v *= scale;
     }
@@ -89,14 +89,40 @@ __global__ void gather_unet_input_k(const f16* __restrict__ rgb, long rgb_ld, co
 }
 
 __global__ void ddim_combine_k(const f16* __restrict__ x, long ldx, const f16* __restrict__ e, long lde,
-                               f16* __restrict__ y, long ldy, long P, int C, int Cpad, float ca, float cb, float sc) {
+                               f16* __restrict__ y, long ldy, long P, int C, int Cpad, float ca, float cb, float sc,
+                               long e_period) {
   long n = P * Cpad;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     long p = i / Cpad;
     int c = (int)(i - p * Cpad);
+    long pe = e_period > 0 ? p % e_period : p;
     float v = 0.f;
-    if (c < C) v = (ca * (float)x[p * ldx + c] + cb * (float)e[p * lde + c]) * sc;
+    if (c < C) v = (ca * (float)x[p * ldx + c] + cb * (float)e[pe * lde + c]) * sc;
     y[p * ldy + c] = (f16)v;
+  }
+}
+
+// refine (rollingdepth_pipeline.py:586-629): new[f] = mean over the snippets s covering f
+// (s = f - j*stride, slot j) of pred[s][j]; accumulated in f32 in snippet order.
+__global__ void snippet_average_k(const f16* __restrict__ src, int n, int w, int stride, long P, int C, int ld,
+                                  f16* __restrict__ out) {
+  const int f = blockIdx.y;
+  const long tot = P * ld;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % ld);
+    float v = 0.f;
+    if (c < C) {
+      float s = 0.f;
+      int cnt = 0;
+      for (int j = w - 1; j >= 0; --j) {  // snippet index ascending
+        const int sn = f - j * stride;
+        if (sn < 0 || sn >= n) continue;
+        s += (float)src[((long)sn * w + j) * tot + i];
+        ++cnt;
+      }
+      v = cnt ? s / (float)cnt : 0.f;
+    }
+    out[(long)f * tot + i] = (f16)v;
   }
 }
 
@@ -149,11 +175,11 @@ __global__ void renorm_k(float* __restrict__ x, long n, const float* __restrict_
 }  // namespace
 
 extern "C" int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int B, int C, int H, int W, int Cpad, float scale,
-                                 void* stream) {
+                                 long x_bstride, long x_cstride, void* stream) {
   RDMI_REQUIRE(x && y && Cpad >= C, RDMI_E_ARG, "nchw_to_nhwc: bad args");
   long n = (long)B * H * W * Cpad;
   hipLaunchKernelGGL(nchw_to_nhwc_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, x_f32, (f16*)y, C,
-                     (long)H * W, Cpad, n, scale);
+                     (long)H * W, Cpad, n, scale, x_bstride, x_cstride);
   return rdmi::check_launch("nchw_to_nhwc");
 }
 
@@ -194,11 +220,11 @@ extern "C" int rdmi_gather_unet_input(const void* rgb, long rgb_frame_ld, const 
 }
 
 extern "C" int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* y, long ld_y, long P, int C,
-                                 int Cpad, float ca, float cb, float out_scale, void* stream) {
+                                 int Cpad, float ca, float cb, float out_scale, long e_period, void* stream) {
   RDMI_REQUIRE(x && e && y && Cpad >= C, RDMI_E_ARG, "ddim_combine: bad args");
   long n = P * Cpad;
   hipLaunchKernelGGL(ddim_combine_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld_x,
-                     (const f16*)e, ld_e, (f16*)y, ld_y, P, C, Cpad, ca, cb, out_scale);
+                     (const f16*)e, ld_e, (f16*)y, ld_y, P, C, Cpad, ca, cb, out_scale, e_period);
   return rdmi::check_launch("ddim_combine");
 }
 
@@ -217,4 +243,15 @@ extern "C" int rdmi_renormalize_f32(float* x, long n, const float* minmax, void*
   RDMI_REQUIRE(x && minmax && n > 0, RDMI_E_ARG, "renormalize: bad args");
   hipLaunchKernelGGL(renorm_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, minmax);
   return rdmi::check_launch("renormalize");
+}
+
+extern "C" int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld, void* out,
+                                    void* stream) {
+  RDMI_REQUIRE(src && out && n > 0 && w > 0 && N > 0 && ld >= C, RDMI_E_ARG, "snippet_average: bad args");
+  long tot = P * ld;
+  long gx = (tot + 255) / 256;
+  if (gx > 4096) gx = 4096;
+  hipLaunchKernelGGL(snippet_average_k, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream, (const f16*)src, n, w,
+                     stride, P, C, ld, (f16*)out);
+  return rdmi::check_launch("snippet_average");
 }

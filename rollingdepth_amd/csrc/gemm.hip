@@ -23,7 +23,7 @@ struct GemmP {
   const float* rowbias; int rpg; long rb_ld;
   float alpha;
   int M, N, K, Kvalid;
-  int geglu, silu;
+  int geglu, silu, vec;
   // convolution (A gathered from NHWC x)
   int IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
 };
@@ -199,60 +199,105 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r
+  // epilogue.  The MFMA ran as Dᵀ = W·Aᵀ, so a lane holds 4 CONSECUTIVE output channels
+  // n = fq*4 + r of one row m = lane&15: bias / time-embedding / residual are read and the
+  // result written as 4-element vectors (8-B f16 / 16-B f32), scalar only at a ragged N tail.
   const long cb = (long)bz * p.sC;
   const long rbz = (long)bz * p.sR;
   if (!p.geglu) {
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+      if (m >= p.M) continue;
+      const float* rbrow = p.rowbias ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
+      const long crow = cb + (long)m * p.ldc;
+      const long rrow = rbz + (long)m * p.ldr;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        if (m >= p.M) continue;
-        const float* rbrow = p.rowbias ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
+      for (int j = 0; j < RN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + fq * 4;
+        if (n >= p.N) continue;
+        float v[4];
 #pragma unroll
-        for (int j = 0; j < RN; ++j) {
-          int n = n0 + wn * WTN + j * 16 + fr;
-          if (n >= p.N) continue;
-          float v = acc[i][j][r] * p.alpha;
-          if (p.bias) v += p.bias[n];
-          if (rbrow) v += rbrow[n];
-          if (p.R) v += (float)p.R[rbz + (long)m * p.ldr + n];
-          if (p.silu) v = silu_f(v);
-          if (p.c_f32)
-            ((float*)p.C)[cb + (long)m * p.ldc + n] = v;
-          else
-            ((f16*)p.C)[cb + (long)m * p.ldc + n] = (f16)v;
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
+        if (p.vec && n + 3 < p.N) {
+          if (p.bias) {
+            const f32x4 bb = *(const f32x4*)(p.bias + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bb[r];
+          }
+          if (rbrow) {
+            const f32x4 bb = *(const f32x4*)(rbrow + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bb[r];
+          }
+          if (p.R) {
+            const f16x4 rr = *(const f16x4*)(p.R + rrow + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+          }
+          if (p.silu) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
+          }
+          if (p.c_f32) {
+            *(f32x4*)((float*)p.C + crow + n) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+            f16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+            *(f16x4*)((f16*)p.C + crow + n) = o;
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = n + r;
+            if (nn >= p.N) break;
+            float x = v[r];
+            if (p.bias) x += p.bias[nn];
+            if (rbrow) x += rbrow[nn];
+            if (p.R) x += (float)p.R[rrow + nn];
+            if (p.silu) x = silu_f(x);
+            if (p.c_f32)
+              ((float*)p.C)[crow + nn] = x;
+            else
+              ((f16*)p.C)[crow + nn] = (f16)x;
+          }
         }
       }
     }
   } else {
     // GEGLU: within each wave's WTN(=64)-column slab, columns [0,32) are the value half and
-    // [32,64) the gate half of output columns slab*32 + [0,32).
+    // [32,64) the gate half of output columns slab*32 + [0,32) (N % 128 == 0: always vector).
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + fr;
+      if (m >= p.M) continue;
+      const long crow = cb + (long)m * p.ldc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int m = m0 + wm * WTM + i * 16 + fq * 4 + r;
-        if (m >= p.M) continue;
+      for (int j = 0; j < RN / 2; ++j) {
+        const int nh = n0 + wn * WTN + j * 16 + fq * 4;
+        const int ng = nh + WTN / 2;
+        const int no = (n0 + wn * WTN) / 2 + j * 16 + fq * 4;
+        float v[4];
 #pragma unroll
-        for (int j = 0; j < RN / 2; ++j) {
-          int nh = n0 + wn * WTN + j * 16 + fr;
-          int ng = nh + WTN / 2;
-          int no = (n0 + wn * WTN) / 2 + j * 16 + fr;
-          float h = acc[i][j][r] * p.alpha + (p.bias ? p.bias[nh] : 0.f);
-          float g = acc[i][j + RN / 2][r] * p.alpha + (p.bias ? p.bias[ng] : 0.f);
-          float v = h * gelu_erf(g);
-          if (p.R) v += (float)p.R[rbz + (long)m * p.ldr + no];
-          if (p.c_f32)
-            ((float*)p.C)[cb + (long)m * p.ldc + no] = v;
-          else
-            ((f16*)p.C)[cb + (long)m * p.ldc + no] = (f16)v;
+        for (int r = 0; r < 4; ++r) {
+          const float h = acc[i][j][r] * p.alpha + (p.bias ? p.bias[nh + r] : 0.f);
+          const float g = acc[i][j + RN / 2][r] * p.alpha + (p.bias ? p.bias[ng + r] : 0.f);
+          v[r] = h * gelu_erf(g);
+          if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
+        }
+        if (p.c_f32) {
+          *(f32x4*)((float*)p.C + crow + no) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          f16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+          *(f16x4*)((f16*)p.C + crow + no) = o;
         }
       }
     }
@@ -286,6 +331,16 @@ int launch(const GemmP& p, int batch, hipStream_t s, bool force128, bool conv) {
 
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// 4-wide epilogue vectors need 4-element-aligned rows and pointers
+bool vec_ok(const GemmP& p) {
+  const uintptr_t csz = p.c_f32 ? 16 : 8;
+  bool ok = p.ldc % 4 == 0 && p.sC % 4 == 0 && ((uintptr_t)p.C % csz) == 0;
+  if (p.R) ok = ok && p.ldr % 4 == 0 && p.sR % 4 == 0 && ((uintptr_t)p.R & 7) == 0;
+  if (p.bias) ok = ok && ((uintptr_t)p.bias & 15) == 0;
+  if (p.rowbias) ok = ok && ((uintptr_t)p.rowbias & 15) == 0 && p.rb_ld % 4 == 0;
+  return ok;
+}
+
 }  // namespace
 
 extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
@@ -308,6 +363,8 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.M = a->M; p.N = a->N; p.K = (a->K + BK - 1) / BK * BK; p.Kvalid = a->K;
   p.geglu = a->epilogue == RDMI_EPI_GEGLU;
   p.silu = a->epilogue == RDMI_EPI_SILU;
+  p.vec = vec_ok(p);
+  RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm: GEGLU output needs 4-element aligned rows");
   return launch(p, a->batch, (hipStream_t)stream, p.geglu, false);
 }
 
@@ -334,5 +391,6 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   const bool dense = a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad_top == 0 && a->pad_left == 0 && !a->upsample &&
                      a->Ho == a->H && a->Wo == a->W;
   if (dense) p.lda = a->Cin;
+  p.vec = vec_ok(p);
   return launch(p, 1, (hipStream_t)stream, false, !dense);
 }

@@ -303,13 +303,15 @@ def transpose(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Te
 
 # ----------------------------------------------------------------------------- layout / misc
 def nchw_to_nhwc(x: torch.Tensor, cpad: int, scale: float = 1.0) -> torch.Tensor:
+    """[B, C, H, W] (any batch/channel strides, e.g. a stride-0 channel repeat) → NHWC f16."""
     if not x.is_cuda or x.dtype not in (F16, F32):
         raise TypeError("nchw_to_nhwc: device f16/f32 tensor expected")
-    x = x.contiguous()
     B, Cc, H, W = x.shape
+    if x.stride(3) != 1 or x.stride(2) != W:
+        x = x.contiguous()
     out = torch.empty((B, H, W, cpad), dtype=F16, device=x.device)
     check(lib.rdmi_nchw_to_nhwc(x.data_ptr(), int(x.dtype == F32), out.data_ptr(), B, Cc, H, W, cpad, scale,
-                                _stream()), "rdmi_nchw_to_nhwc")
+                                x.stride(0), x.stride(1), _stream()), "rdmi_nchw_to_nhwc")
     return out
 
 
@@ -347,12 +349,28 @@ def gather_unet_input(rgb: torch.Tensor, depth: torch.Tensor, frame_idx: torch.T
 
 def ddim_combine(x: torch.Tensor, e: torch.Tensor, ca: float, cb: float, out_scale: float, c: int, cpad: int,
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """y[..., :c] = (ca·x + cb·e)·out_scale, y[..., c:cpad] = 0; x/e [P, ld] channel-last views."""
+    """y[..., :c] = (ca·x + cb·e)·out_scale, y[..., c:cpad] = 0; x/e channel-last views [.., P, ld].
+    If e has fewer pixel rows than x (e.g. one noise frame), it is broadcast periodically."""
     P = x.numel() // x.shape[-1]
+    Pe = e.numel() // e.shape[-1]
+    period = 0 if Pe == P else Pe
+    if period and P % Pe:
+        raise ValueError("ddim_combine: broadcast operand must tile the sample")
     out = torch.empty((*x.shape[:-1], cpad), dtype=F16, device=x.device) if out is None else out
     check(lib.rdmi_ddim_combine(x.data_ptr(), x.stride(-2) if x.dim() >= 2 else x.shape[-1], e.data_ptr(),
                                 e.stride(-2) if e.dim() >= 2 else e.shape[-1], out.data_ptr(), out.stride(-2), P, c, cpad,
-                                ca, cb, out_scale, _stream()), "rdmi_ddim_combine")
+                                ca, cb, out_scale, period, _stream()), "rdmi_ddim_combine")
+    return out
+
+
+def snippet_average(src: torch.Tensor, stride: int, N: int, c: int = 4) -> torch.Tensor:
+    """src [n, w, h, wd, ld] f16 → [N, h, wd, ld] mean over covering snippets (refine)."""
+    _need(src, F16, "snippet_average.src")
+    n, w, h, wd, ld = src.shape
+    src = src.contiguous()
+    out = torch.empty((N, h, wd, ld), dtype=F16, device=src.device)
+    check(lib.rdmi_snippet_average(src.data_ptr(), n, w, stride, N, h * wd, c, ld, out.data_ptr(), _stream()),
+          "rdmi_snippet_average")
     return out
 
 

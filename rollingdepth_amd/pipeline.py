@@ -230,6 +230,37 @@ class RollingDepthPipeline:
             outs.append(buf)
         return outs
 
+    def refine(self, rgb_latent: torch.Tensor, depth_latents: torch.Tensor, init_noise: torch.Tensor,
+               refine_step: int, snippet_len: int, start_dilation: int, skip_t_ratio: float = 0.5) -> torch.Tensor:
+        """rollingdepth_pipeline.py:517-633 on device.  rgb_latent / depth_latents NHWC [N,h,w,8]
+        (channels 0..3), init_noise NHWC [1,h,w,8].  Returns the refined latents [N,h,w,8]."""
+        self._context()
+        N, h, w, _ = rgb_latent.shape
+        T = int(refine_step / skip_t_ratio)
+        assert T <= self.scheduler.config["num_train_timesteps"], "Too many refinement steps"
+        self.scheduler.set_timesteps(T)
+        timesteps = self.scheduler.timesteps
+        start = int(len(timesteps) * skip_t_ratio)
+        ts = timesteps[start:].tolist()
+        assert 0 < len(ts) < T, f"invalid {skip_t_ratio = }"
+        sa, sb = self.scheduler.add_noise_coefficients(ts[0])
+        new = K.ddim_combine(depth_latents[..., :4], init_noise[..., :4], sa, sb, 1.0, 4, 8)
+        for i_step, t in enumerate(ts):
+            idx = self.get_snippet_indice(i_step, ts, N, snippet_len, start_dilation, 1, 1)
+            stride = idx[0][1] - idx[0][0] if snippet_len > 1 else 1
+            preds = torch.empty((len(idx), snippet_len, h, w, 8), dtype=F16, device=self.device)
+            for b0 in range(0, len(idx), self.snippet_batch):
+                sel = idx[b0:b0 + self.snippet_batch]
+                fidx = torch.tensor([f for s in sel for f in s], dtype=torch.int32, device=self.device)
+                x = K.gather_unet_input(rgb_latent, new, fidx, depth_bcast=False)
+                pred = self.unet.forward(x, int(t), num_view=snippet_len)
+                self.scheduler.step_(pred, int(t), x[..., 4:8], 1.0, channels=4,
+                                     out=preds[b0:b0 + len(sel)].view(len(sel) * snippet_len, h, w, 8))
+            covered = {f for s in idx for f in s}
+            assert len(covered) == N, "refine: every frame must be covered by a snippet"
+            new = K.snippet_average(preds, stride, N)
+        return new
+
     # ------------------------------------------------------------------ entry points
     @torch.no_grad()
     def __call__(self, input_video_path, start_frame: int = 0, frame_count: int = 0, processing_res: int = 1024,
@@ -283,8 +314,6 @@ class RollingDepthPipeline:
             for i, d in enumerate(dilations):
                 dilations[i] = self.cap_max_dilation(seq_len, snippet_lengths[i], d, verbose)
             refine_start_dilation = self.cap_max_dilation(seq_len, refine_snippet_len, refine_start_dilation, verbose)
-        if refine_step > 0:
-            raise NotImplementedError("refine (full/paper presets) is the next row (SURVEY.md §8f rank 1)")
         if input_frames.shape[0] != 1:
             raise NotImplementedError("Layered inference is only implemented for B=1")
         # ----------------- encode (H2D boundary :263)
@@ -304,11 +333,23 @@ class RollingDepthPipeline:
                                                   dilations)
         d = merged.float().contiguous()
         K.renormalize_(d, K.minmax(d))
-        depth = d.to(F16)
+        coaligned = d.to(F16)
         if record is not None:
             record.update(rgb_latent=rgb_latent, scales=scales, translations=trans, loss_history=hist,
                           dilations=list(dilations))
+        # ----------------- refinement (:323-343, full/paper presets)
+        if refine_step > 0:
+            dlat = self.encode_rgb(coaligned.expand(-1, 3, -1, -1))
+            new = self.refine(rgb_latent, dlat, noise, refine_step, refine_snippet_len, refine_start_dilation)
+            if record is not None:
+                record["refined_latent"] = new
+            z = K.ddim_combine(new[..., :4], new[..., :4], 1.0 / self.depth_latent_scale_factor, 0.0, 1.0, 4, 8)
+            dec = torch.empty((N, H, W, 1), dtype=F16, device=self.device)
+            self.decode_depth(z, dec)
+            depth = dec.view(N, 1, H, W)
+        else:
+            depth = coaligned
         # ----------------- outputs (:345-353, D2H boundary)
         snip_out = [s.view(s.shape[0], s.shape[1], 1, H, W).cpu() for s in snippets]
         return RollingDepthOutput(input_rgb=input_frames[0].float().cpu() / 2.0 + 0.5, depth_pred=depth.cpu(),
-                                  snippet_ls=snip_out, depth_coaligned=depth.cpu())
+                                  snippet_ls=snip_out, depth_coaligned=coaligned.cpu())

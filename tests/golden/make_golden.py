@@ -53,7 +53,7 @@ def build_pipe(P, ucfg, vcfg, scfg, seed=0):
     return pipe
 
 
-def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None):
+def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step=0, refine_start=6):
     rec = {"unet_out": [], "snip_lat": []}
     orig_single = pipe.single_step
     orig_dec = pipe.decode_depth
@@ -81,30 +81,33 @@ def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None):
     with torch.no_grad():
         out = pipe.forward(
             input_frames=frames[None], dilations=dil, cap_dilation=cap, snippet_lengths=[3],
-            init_infer_steps=[1], strides=[1], coalign_kwargs=coalign, refine_step=0,
-            refine_snippet_len=3, refine_start_dilation=6, generator=g, verbose=False,
+            init_infer_steps=[1], strides=[1], coalign_kwargs=coalign, refine_step=refine_step,
+            refine_snippet_len=3, refine_start_dilation=refine_start, generator=g, verbose=False,
             max_vae_bs=4, unload_snippet=False)
     rec["dilations_used"] = dil  # forward mutates the caller's list in place (:246-252)
     return out, rec
 
 
-def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None):
+def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, refine_step=0, refine_start=6):
     pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
     h, w = frames.shape[-2] // C.vae_downscale(vcfg), frames.shape[-1] // C.vae_downscale(vcfg)
     noise = torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(1))
-    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign)
+    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign, refine_step, refine_start)
     t = {
         "frames": _c(frames), "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
         "rgb_latent": rec["rgb_latent"], "depth_pred": _c(out.depth_pred),
         "depth_coaligned": _c(out.depth_coaligned),
         "unet_out_first": rec["unet_out"][0].clone(), "unet_out_last": rec["unet_out"][-1].clone(),
     }
+    if refine_step > 0:
+        t["refined_latent"] = rec["snip_lat"][-1][0].clone()  # decode_depth's input after refine
     for i, (lat, sn) in enumerate(zip(rec["snip_lat"], out.snippet_ls)):
         t[f"snippet_latent_{i}"] = lat
         t[f"snippet_{i}"] = _c(sn)
     save_file(t, os.path.join(HERE, name + ".safetensors"))
     meta = {"dilations_in": list(dilations), "dilations_used": rec["dilations_used"], "cap_dilation": cap,
-            "unet": ucfg, "vae": vcfg, "scheduler": C.RD_SCHEDULER, "coalign": coalign or {}}
+            "unet": ucfg, "vae": vcfg, "scheduler": C.RD_SCHEDULER, "coalign": coalign or {},
+            "refine_step": refine_step, "refine_start_dilation": refine_start}
     json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
     print(name, {k: tuple(v.shape) for k, v in t.items()})
 
@@ -239,7 +242,7 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
     P, A = _refload.load_reference()
-    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "sd2"]
+    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "sd2"]
     if "keys" in todo:
         keys_fixture()
     if "idx" in todo:
@@ -253,6 +256,10 @@ def main():
     if "tiny" in todo:
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_pipeline", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True)
+    if "refine" in todo:
+        frames = W.synth_frames(9, 32, 32, seed=0)
+        pipeline_fixture(P, "tiny_refine", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, refine_step=2,
+                         refine_start=6)
     if "sd2" in todo and not a.skip_sd2:
         frames = W.synth_frames(3, 256, 256, seed=0)
         pipeline_fixture(P, "sd2_256", C.SD2_UNET, C.SD2_VAE, frames, [1], False)

@@ -107,13 +107,17 @@ def _pipeline_check(name, tol_lat, tol_depth):
     rec = {}
     with torch.no_grad():
         d = O.pipeline_forward(usd, ucfg, vsd, vcfg, meta["scheduler"], t["frames"], t["init_noise"], t["context"],
-                               meta["dilations_in"], meta["cap_dilation"], coalign_kwargs=meta["coalign"], record=rec)
+                               meta["dilations_in"], meta["cap_dilation"], coalign_kwargs=meta["coalign"], record=rec,
+                               refine_step=meta.get("refine_step", 0),
+                               refine_start_dilation=meta.get("refine_start_dilation", 6))
     assert rec["dilations"] == meta["dilations_used"]
     torch.testing.assert_close(rec["rgb_latent"], t["rgb_latent"], rtol=0, atol=tol_lat)
     for i in range(len(rec["snippets"])):
         torch.testing.assert_close(rec["snippet_latents"][i].reshape(t[f"snippet_latent_{i}"].shape),
                                    t[f"snippet_latent_{i}"], rtol=0, atol=tol_lat)
         torch.testing.assert_close(rec["snippets"][i], t[f"snippet_{i}"], rtol=0, atol=tol_lat)
+    if "refined_latent" in t:
+        torch.testing.assert_close(rec["refined_latent"], t["refined_latent"], rtol=0, atol=10 * tol_lat)
     # north_star parity metric: per-pixel depth L1 (mean |Δ|) ≤ tol_depth; the aligner's Adam
     # trajectory decorrelates at f32 rounding (see test_aligner_oracle_vs_reference), so the max
     # is bounded separately and loosely.
@@ -124,6 +128,13 @@ def _pipeline_check(name, tol_lat, tol_depth):
 
 def test_tiny_pipeline_oracle_vs_reference():
     _pipeline_check("tiny_pipeline", 1e-4, 1e-3)
+
+
+def test_tiny_refine_oracle_vs_reference():
+    """refine (rollingdepth_pipeline.py:517-633, full/paper presets): re-encode the co-aligned depth,
+    add noise at the middle timestep, 1 further denoise pass per remaining timestep with shrinking
+    gaps, per-frame averaging, decode."""
+    _pipeline_check("tiny_refine", 1e-4, 1e-3)
 
 
 @pytest.mark.slow

@@ -23,8 +23,9 @@ def _run(name, snippet_batch=8):
     pipe.empty_text_embed = t["context"]
     rec = {}
     dil = list(meta["dilations_in"])
-    out = pipe.forward(t["frames"][None], dil, meta["cap_dilation"], [3], [1], [1], meta["coalign"] or None, 0, 3, 6,
-                       None, False, 4, False, init_noise=t["init_noise"], record=rec)
+    out = pipe.forward(t["frames"][None], dil, meta["cap_dilation"], [3], [1], [1], meta["coalign"] or None,
+                       meta.get("refine_step", 0), 3, meta.get("refine_start_dilation", 6), None, False, 4, False,
+                       init_noise=t["init_noise"], record=rec)
     return t, meta, out, rec, dil
 
 
@@ -51,6 +52,20 @@ def _check(name, tol_lat_rel, tol_depth_l1):
     print(f"{name} depth L1 {m:.2e} max {mx:.2e}")
     assert m <= tol_depth_l1
     assert out.depth_pred.shape == t["depth_pred"].shape
+
+
+def test_tiny_refine_vs_reference_golden():
+    """full/paper-preset refine stage (rollingdepth_pipeline.py:517-633) on the HIP path."""
+    t, meta, out, rec, dil = _run("tiny_refine")
+    got = rec["refined_latent"][..., :4].permute(0, 3, 1, 2).float().cpu()
+    m, mx, ref = _stats(got, t["refined_latent"])
+    print(f"tiny_refine refined latent mean {m:.2e} max {mx:.2e} (|ref| {ref:.2f})")
+    assert mx <= 2e-2 * ref
+    m, mx, ref = _stats(out.depth_pred, t["depth_pred"])
+    print(f"tiny_refine depth L1 {m:.2e} max {mx:.2e}")
+    assert m <= 1e-2
+    m, mx, ref = _stats(out.depth_coaligned, t["depth_coaligned"])
+    assert m <= 1e-2
 
 
 def test_tiny_pipeline_vs_reference_golden():
