@@ -1,7 +1,7 @@
 // Cross-frame attention kernels.
 //
 // attn_fwd_d64: flash-style fused softmax(q kᵀ·scale) v for head_dim 64 on gfx950.
-//   Workgroup = 8 waves × 32 queries (256 queries) of one (batch, head); 64-key K/V tiles arrive
+//   Workgroup = 8 waves × 32 queries (256 queries) of one (batch, head); 128-key K/V tiles arrive
 //   by LDS-DMA into a 3-slot ring (two tiles in flight; K XOR-swizzled per 16-B chunk through the
 //   source address).
 //   Per wave and tile: Sᵀ = K·Qᵀ with v_mfma_f32_32x32x16_f16 (Q fragments live in registers for
@@ -27,7 +27,9 @@ struct AttnP {
 
 constexpr int NWV = 8;        // waves per workgroup
 constexpr int QB = 32 * NWV;  // queries per workgroup (32 per wave)
-constexpr int KB = 64;        // keys per tile
+constexpr int KB = 128;       // keys per tile
+constexpr int NKB = KB / 32;  // 32-key MFMA blocks per tile
+constexpr int DPW = KB / 8 / NWV;  // 8-row DMA instructions per wave per tile, per tensor
 constexpr int TILE = KB * 64; // halves per K (or V) tile
 
 __device__ f16x8 g_attn_zero16;
@@ -42,7 +44,7 @@ __device__ __forceinline__ void attn_wait_vmcnt() {
 // XOR-swizzled by (key & 7) through the per-lane source address; V stays row-major for the
 // transposed reads.
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
-  __shared__ __attribute__((aligned(16))) f16 lds[3 * 2 * TILE];  // 48 KB: slot s = [K | V]
+  __shared__ __attribute__((aligned(16))) f16 lds[3 * 2 * TILE];  // 96 KB: slot s = [K | V]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -64,19 +66,26 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     qf[ks] = qi < p.Sq ? *(const f16x8*)(Q + (long)qi * p.q_ld + ks * 16 + hh * 8) : z;
   }
 
-  // DMA lane geometry: 8 rows x 8 chunks per 1-KiB instruction
+  // DMA lane geometry: 8 rows x 8 chunks per 1-KiB instruction; row = wid*8 + drow.
+  // LDS images (bank-conflict-free for the fragment reads, checked with SQ_LDS_BANK_CONFLICT):
+  //   K: phys chunk = logical ^ ((row >> 1) & 7)   (ds_read_b128 of 16 distinct rows / group)
+  //   V: phys chunk = logical ^ (((row >> 1) & 1) << 2)   (tr reads of 4 rows x 64 B / half-wave)
   const int drow = lane >> 3;
-  const int kchunk = (lane & 7) ^ drow;  // K: logical chunk stored at phys (lane & 7)
-  const int vchunk = lane & 7;
   const f16* zero = (const f16*)&g_attn_zero16;
   auto issue = [&](int kt, int slot) {
-    const int key = kt * KB + wid * 8 + drow;
-    const bool ok = key < p.Sk;
-    f16* ks_ = lds + slot * 2 * TILE + wid * 8 * 64;
-    __builtin_amdgcn_global_load_lds(ok ? (const void*)(K + (long)key * p.k_ld + kchunk * 8) : (const void*)zero,
-                                     (__attribute__((address_space(3))) void*)ks_, 16, 0, 0);
-    __builtin_amdgcn_global_load_lds(ok ? (const void*)(V + (long)key * p.v_ld + vchunk * 8) : (const void*)zero,
-                                     (__attribute__((address_space(3))) void*)(ks_ + TILE), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int row = (i * NWV + wid) * 8 + drow;  // (row >> 1) & 7 depends on drow and wid only
+      const int kchunk = (lane & 7) ^ ((row >> 1) & 7);
+      const int vchunk = (lane & 7) ^ (((row >> 1) & 1) << 2);
+      const int key = kt * KB + row;
+      const bool ok = key < p.Sk;
+      f16* ks_ = lds + slot * 2 * TILE + (i * NWV + wid) * 8 * 64;
+      __builtin_amdgcn_global_load_lds(ok ? (const void*)(K + (long)key * p.k_ld + kchunk * 8) : (const void*)zero,
+                                       (__attribute__((address_space(3))) void*)ks_, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(ok ? (const void*)(V + (long)key * p.v_ld + vchunk * 8) : (const void*)zero,
+                                       (__attribute__((address_space(3))) void*)(ks_ + TILE), 16, 0, 0);
+    }
   };
 
   f32x16 o[2];
@@ -92,27 +101,27 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   const int tr_key = 4 * (gi >> 1) + (li >> 2);
   const int tr_col = 16 * (gi & 1) + 4 * (li & 3);
   issue(0, 0);
-  issue(1, 1);  // zero rows when nt == 1: keeps exactly 2 younger DMAs in flight at every wait
+  issue(1, 1);  // zero rows when nt == 1: keeps exactly 2·DPW younger DMAs in flight at every wait
 
   for (int kt = 0; kt < nt; ++kt) {
-    attn_wait_vmcnt<2>();  // this wave's DMAs of tile kt landed (tile kt+1 in flight)
+    attn_wait_vmcnt<2 * DPW>();  // this wave's DMAs of tile kt landed (tile kt+1 in flight)
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave's DMAs of kt landed; every wave done with kt-1
     asm volatile("" ::: "memory");
     issue(kt + 2, (kt + 2) % 3);   // past the end: zero rows into the drained slot
     const f16* ks_ = lds + (kt % 3) * 2 * TILE;
     const f16* vs_ = ks_ + TILE;
-    // ---- Sᵀ = K · Qᵀ for 2 key blocks of 32
-    f32x16 s[2];
+    // ---- Sᵀ = K · Qᵀ for NKB key blocks of 32
+    f32x16 s[NKB];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < NKB; ++kb) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
       const int key = kb * 32 + c;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int ch = 2 * ks + hh;
-        f16x8 kf = *(const f16x8*)(ks_ + key * 64 + ((ch ^ (key & 7)) << 3));
+        f16x8 kf = *(const f16x8*)(ks_ + key * 64 + ((ch ^ ((key >> 1) & 7)) << 3));
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], s[kb], 0, 0, 0);
       }
     }
@@ -121,12 +130,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     float mx = -INFINITY;
     if (kbase + KB <= p.Sk) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
     } else {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -138,7 +147,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     const float mn = fmaxf(m, mx);
     // exact T13: rescale O only when some lane's running max moved (alpha == 1 otherwise)
     if (__any(mn > m)) {
-      const float alpha = exp2f((m - mn) * p.sl2);
+      const float alpha = __builtin_amdgcn_exp2f((m - mn) * p.sl2);
       l *= alpha;
 #pragma unroll
       for (int d = 0; d < 2; ++d)
@@ -148,28 +157,28 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     }
     const float msc = m * p.sl2;
     float rs = 0.f;
-    f16x8 pf[4];
+    f16x8 pf[2 * NKB];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float e = exp2f(fmaf(s[kb][r], p.sl2, -msc));
+        float e = __builtin_amdgcn_exp2f(fmaf(s[kb][r], p.sl2, -msc));  // v_exp_f32, no denorm fixup
         rs += e;
         pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
       }
     l += rs;
-    // ---- Oᵀ += Vᵀ · Pᵀ (4 k-steps of 16 keys, 2 d-blocks of 32)
+    // ---- Oᵀ += Vᵀ · Pᵀ (KB/16 k-steps of 16 keys, 2 d-blocks of 32)
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
+    for (int st = 0; st < 2 * NKB; ++st) {
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
-        const f16* base = vs_ + (16 * st + tr_key) * 64 + d * 32 + tr_col;
+        // row = 16st + tr_key (+8): (row >> 1) & 1 == (tr_key >> 1) & 1 for both reads
+        const int col = d * 32 + tr_col;
+        const int pc = ((col >> 3) ^ (((tr_key >> 1) & 1) << 2)) << 3 | (col & 7);
+        const f16* base = vs_ + (16 * st + tr_key) * 64 + pc;
         i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, base));
         i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, base + 8 * 64));
-        f16x8 vf;
-        f16x4 lo4 = *(f16x4*)&lo, hi4 = *(f16x4*)&hi;
-        vf[0] = lo4[0]; vf[1] = lo4[1]; vf[2] = lo4[2]; vf[3] = lo4[3];
-        vf[4] = hi4[0]; vf[5] = hi4[1]; vf[6] = hi4[2]; vf[7] = hi4[3];
+        const f16x8 vf = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[st], o[d], 0, 0, 0);
       }
     }
