@@ -24,15 +24,10 @@ struct GemmP {
   float alpha;
   int M, N, K, Kvalid;
   int geglu, silu, vec;
+  unsigned a_bytes, w_bytes;  // operand extents for the buffer descriptors (OOB lanes read 0)
   // convolution (A gathered from NHWC x)
   int IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
 };
-
-__device__ f16x8 g_zero16;  // source of the zero chunks (padding / out-of-range) for LDS-DMA
-
-__device__ __forceinline__ void glds16(const void* g, f16* l) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
-}
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
 template <int N>
@@ -40,11 +35,20 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-// MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x (kh×kw conv).
-// Operands reach LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging, no ds_write) into a
-// 3-slot ring of [rows][64-half] tiles, two K-steps in flight, one barrier per K-step.  Each
+constexpr unsigned OOB = 0x80000000u;  // byte offset past every descriptor's extent → zeros
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f16* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, 0, 0, 0);
+}
+
+// MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x for a 3×3 conv
+// (any stride/padding); MODE 2: 3×3 conv reading x through a nearest ×2 upsample.
+// Operands reach LDS by LDS-DMA (buffer_load_dwordx4 … lds: no VGPR staging, no ds_write) into a
+// 3-slot ring of [rows][64-half] tiles, two K-steps in flight, one barrier per K-step.  Padding,
+// ragged M/N/K and the implicit zero padding of the conv all become out-of-range buffer offsets,
+// which the descriptor's range check turns into zero chunks (no select, no zero buffer).  Each
 // 1-KiB DMA instruction fills 8 rows lane-linearly; the 16-B chunk swizzle (phys = logical ^
-// (row & 7)) is applied on the per-lane SOURCE address and on the fragment read (guide rule 21),
+// (row & 7)) is applied on the per-lane SOURCE offset and on the fragment read (guide rule 21),
 // so ds_read_b128 fragment reads are conflict-free.
 template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
@@ -75,50 +79,51 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
   const int n0 = (logical % nbx) * BN;
   const int m0 = (logical / nbx) * BM;
   const int bz = blockIdx.z;
-  const f16* A = p.A + (long)bz * p.sA;
-  const f16* Wt = p.Wt + (long)bz * p.sW;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)bz * p.sA), (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.Wt + (long)bz * p.sW), (short)0, (int)p.w_bytes, 0x00020000);
 
   // lane → (row within its 8-row DMA group, logical chunk): phys chunk = lane & 7
   const int lrow = lane >> 3;
   const int chunk = (lane & 7) ^ lrow;
-  // element offsets are 32-bit (every operand of this path is < 2^31 elements; checked on host)
-  bool arow_ok[AV];
-  int abase[AV];
-  int ahb[AV], awb[AV];
+  // per A row: element offset of the tap-(0,0) input pixel (MODE 1), or of the row (MODE 0);
+  // rows past M get hb = INT_MIN/2 so every bounds check fails
+  int arow[AV], ahb[AV], awb[AV];
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
     const int m = m0 + (i * NW + wid) * 8 + lrow;
-    arow_ok[i] = m < p.M;
-    const int mm = arow_ok[i] ? m : 0;
-    if (MODE == 1) {
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    if (MODE != 0) {
       const int hw = p.Ho * p.Wo;
       const int b = mm / hw;
       const int r = mm - b * hw;
       const int ho = r / p.Wo;
       const int wo = r - ho * p.Wo;
-      ahb[i] = ho * p.stride - p.pt;
+      const int hb = ho * p.stride - p.pt;
+      ahb[i] = ok ? hb : -(1 << 28);  // rows past M fail every bounds check
       awb[i] = wo * p.stride - p.pl;
-      abase[i] = b * p.IH * p.IW * p.Cin;
+      arow[i] = MODE == 1 ? (b * p.IH + hb) * p.IW * p.Cin + awb[i] * p.Cin  // may be < 0: only used when valid
+                          : b * p.IH * p.IW * p.Cin;
     } else {
-      abase[i] = mm * (int)p.lda;
-      ahb[i] = awb[i] = 0;
+      ahb[i] = ok ? 0 : -1;
+      awb[i] = 0;
+      arow[i] = mm * (int)p.lda;
     }
   }
-  bool brow_ok[BV];
-  int bbase[BV];
+  int brow[BV];
 #pragma unroll
   for (int i = 0; i < BV; ++i) {
     const int n = n0 + (i * NW + wid) * 8 + lrow;
-    brow_ok[i] = n < p.N;
-    bbase[i] = (brow_ok[i] ? n : 0) * (int)p.ldw;
+    brow[i] = n < p.N ? n * (int)p.ldw : -1;
   }
   int tap = 0, cv = chunk;
-  if (MODE == 1) {
+  if (MODE != 0) {
     tap = chunk / p.cin_vecs;
     cv = chunk - tap * p.cin_vecs;
   }
-  const int Hl = p.IH << p.up, Wl = p.IW << p.up;
-  const f16* zero = (const f16*)&g_zero16;
+  const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
 
   // issue the DMA of K-step `ks` into ring slot `slot`
   auto issue = [&](int ks, int slot) {
@@ -129,25 +134,23 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
     if (MODE == 0) {
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
-        const bool ok = arow_ok[i] && kok;
-        glds16(ok ? A + (abase[i] + kk) : zero, la + (i * NW + wid) * 8 * BK);
+        const bool ok = ahb[i] == 0 && kok;
+        dma16(ra_, ok ? (unsigned)(arow[i] + kk) * 2u : OOB, la + (i * NW + wid) * 8 * BK);
       }
     } else {
-      int dy, dx;
-      if (p.kw == 3) {
-        dy = (tap * 11) >> 5;  // tap / 3 for tap < 9
-        dx = tap - 3 * dy;
-      } else {
-        dy = tap / p.kw;
-        dx = tap - dy * p.kw;
-      }
-      const int coff = cv * 8;
+      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9 (3×3 kernels only)
+      const int dx = tap - 3 * dy;
+      const int tapoff = (dy * p.IW + dx) * p.Cin + cv * 8;
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
         const int hi = ahb[i] + dy, wi = awb[i] + dx;
-        const bool ok = arow_ok[i] && kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
-        const int off = abase[i] + ((hi >> p.up) * p.IW + (wi >> p.up)) * p.Cin + coff;
-        glds16(ok ? A + off : zero, la + (i * NW + wid) * 8 * BK);
+        const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
+        int off;
+        if (MODE == 1)
+          off = arow[i] + tapoff;
+        else
+          off = arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cv * 8;
+        dma16(ra_, ok ? (unsigned)off * 2u : OOB, la + (i * NW + wid) * 8 * BK);
       }
       cv += 8;
       while (cv >= p.cin_vecs) {
@@ -157,8 +160,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      const bool ok = brow_ok[i] && kok;
-      glds16(ok ? Wt + (bbase[i] + kk) : zero, lb + (i * NW + wid) * 8 * BK);
+      const bool ok = brow[i] >= 0 && kok;
+      dma16(rw_, ok ? (unsigned)(brow[i] + kk) * 2u : OOB, lb + (i * NW + wid) * 8 * BK);
     }
   };
 
@@ -321,8 +324,10 @@ void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
   }
 }
 
-int launch(const GemmP& p, int batch, hipStream_t s, bool force128, bool conv) {
-  if (conv)
+int launch(const GemmP& p, int batch, hipStream_t s, bool force128, int mode) {
+  if (mode == 2)
+    launch_mode<2>(p, batch, s, force128);
+  else if (mode == 1)
     launch_mode<1>(p, batch, s, force128);
   else
     launch_mode<0>(p, batch, s, force128);
@@ -351,8 +356,8 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   RDMI_REQUIRE(al16(a->A) && al16(a->W) && a->strideA % 8 == 0 && a->strideW % 8 == 0, RDMI_E_ALIGN, "gemm: A/W not 16-byte aligned");
   RDMI_REQUIRE(a->epilogue != RDMI_EPI_GEGLU || a->N % 128 == 0, RDMI_E_ARG, "gemm: GEGLU needs N %% 128 == 0");
   RDMI_REQUIRE(!a->rowbias || a->rows_per_group > 0, RDMI_E_ARG, "gemm: rowbias needs rows_per_group");
-  RDMI_REQUIRE((long)a->M * a->lda < (1L << 31) && (long)a->N * a->ldw < (1L << 31), RDMI_E_ARG,
-               "gemm: operand exceeds 2^31 elements per batch");
+  RDMI_REQUIRE((long)a->M * a->lda < (1L << 30) && (long)a->N * a->ldw < (1L << 30), RDMI_E_ARG,
+               "gemm: operand exceeds 2^30 elements (2 GiB) per batch");
   GemmP p{};
   p.A = (const f16*)a->A; p.lda = a->lda; p.sA = a->strideA;
   p.Wt = (const f16*)a->W; p.ldw = a->ldw; p.sW = a->strideW;
@@ -365,7 +370,9 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.silu = a->epilogue == RDMI_EPI_SILU;
   p.vec = vec_ok(p);
   RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm: GEGLU output needs 4-element aligned rows");
-  return launch(p, a->batch, (hipStream_t)stream, p.geglu, false);
+  p.a_bytes = (unsigned)(((long)(a->M - 1) * a->lda + a->K) * 2);
+  p.w_bytes = (unsigned)(((long)(a->N - 1) * a->ldw + a->K) * 2);
+  return launch(p, a->batch, (hipStream_t)stream, p.geglu, 0);
 }
 
 extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
@@ -375,8 +382,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   const int K = a->kh * a->kw * a->Cin;
   RDMI_REQUIRE(a->Kp >= K && a->Kp % 8 == 0, RDMI_E_ARG, "conv2d: Kp (%d) must be >= %d and a multiple of 8", a->Kp, K);
   RDMI_REQUIRE(al16(a->x) && al16(a->w), RDMI_E_ALIGN, "conv2d: x/w not 16-byte aligned");
-  RDMI_REQUIRE((long)a->B * a->H * a->W * a->Cin < (1L << 31) && (long)a->Cout * a->Kp < (1L << 31), RDMI_E_ARG,
-               "conv2d: input exceeds 2^31 elements (split the batch)");
+  RDMI_REQUIRE((long)a->B * a->H * a->W * a->Cin < (1L << 30) && (long)a->Cout * a->Kp < (1L << 30), RDMI_E_ARG,
+               "conv2d: input exceeds 2^30 elements (2 GiB; split the batch)");
   GemmP p{};
   p.A = (const f16*)a->x; p.Wt = (const f16*)a->w; p.ldw = a->Kp;
   p.C = a->y; p.ldc = a->y_ld > 0 ? a->y_ld : a->Cout;
@@ -391,6 +398,10 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   const bool dense = a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad_top == 0 && a->pad_left == 0 && !a->upsample &&
                      a->Ho == a->H && a->Wo == a->W;
   if (dense) p.lda = a->Cin;
+  RDMI_REQUIRE(dense || (a->kh == 3 && a->kw == 3), RDMI_E_UNSUPPORTED, "conv2d: only 3x3 and dense 1x1 kernels");
+  RDMI_REQUIRE(!a->upsample || a->stride == 1, RDMI_E_UNSUPPORTED, "conv2d: upsample needs stride 1");
   p.vec = vec_ok(p);
-  return launch(p, 1, (hipStream_t)stream, false, !dense);
+  p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 2);
+  p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 2);
+  return launch(p, 1, (hipStream_t)stream, false, dense ? 0 : (a->upsample ? 2 : 1));
 }
