@@ -99,14 +99,19 @@ def main():
     pipe.snippet_batch = a.snippet_batch
     pipe.vae_batch = a.vae_batch
     N = a.frames * world
-    frames = W.synth_frames(N, a.res, a.res, seed=0)[None].to(dev, torch.float16)
+    from rollingdepth_amd.shard import chunk_bounds
+    if world > 1:  # each rank materialises only its own chunk of the synthetic video
+        lo, hi = chunk_bounds(N, world)[rank]
+        frames = W.synth_frames(N, a.res, a.res, seed=0, first=lo, count=hi - lo).to(dev, torch.float16)
+    else:
+        frames = W.synth_frames(N, a.res, a.res, seed=0)[None].to(dev, torch.float16)
     noise = W.synth_noise(a.res // 8, a.res // 8).to(dev)
     dil0 = [int(x) for x in a.dilations.split(",")]
     coalign = {"num_iterations": a.aligner_iters}
 
     def step():
         if world > 1:
-            return sharded_forward(pipe, frames, list(dil0), True, 3, coalign, init_noise=noise)
+            return sharded_forward(pipe, frames, list(dil0), True, 3, coalign, init_noise=noise, num_frames=N)
         return pipe.forward(frames, list(dil0), True, [3], [1], [1], coalign, 0, 3, 6, None, False, 4, False,
                             init_noise=noise)
 

@@ -75,9 +75,14 @@ def gather_snippets(local: torch.Tensor, counts: Sequence[int], world: int, grou
 
 @torch.no_grad()
 def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool = True,
-                    snippet_len: int = 3, coalign_kwargs=None, init_noise: torch.Tensor = None, group=None):
+                    snippet_len: int = 3, coalign_kwargs=None, init_noise: torch.Tensor = None, group=None,
+                    num_frames: int = None):
     """Multi-GPU RollingDepthPipeline.forward (refine_step = 0).  Returns the depth [N,1,H,W] f16
-    on rank 0 (None elsewhere) and the per-dilation snippets on rank 0."""
+    on rank 0 (None elsewhere) and the per-dilation snippets on rank 0.
+
+    `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N`
+    — only this rank's contiguous chunk chunk_bounds(N, world)[rank] (each rank then holds 1/W of
+    the video in host/device memory)."""
     from . import kernels as K
     from .aligner import DepthAligner
 
@@ -85,7 +90,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     rank = dist.get_rank(group)
     dev = pipe.device
     frames = input_frames[0] if input_frames.dim() == 5 else input_frames
-    N = frames.shape[0]
+    N = frames.shape[0] if num_frames is None else num_frames
     dil = list(dilations)
     if cap_dilation:
         dil = [pipe.cap_max_dilation(N, snippet_len, d) for d in dil]
@@ -94,8 +99,11 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     f = pipe.vae.factor
     H, W = frames.shape[-2:]
     h, w = H // f, W // f
+    mine_frames = frames[lo:hi] if num_frames is None else frames
+    if num_frames is not None and mine_frames.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank} holds {mine_frames.shape[0]} frames, expected {hi - lo}")
     if hi > lo:
-        mine = pipe.encode_rgb(frames[lo:hi].to(dev))
+        mine = pipe.encode_rgb(mine_frames.to(dev))
     else:
         mine = torch.zeros((0, h, w, 8), dtype=F16, device=dev)
     rgb_latent = _all_gather_rows(mine, N, world, group)

@@ -183,17 +183,23 @@ def synth_context(cross_dim: int, seed: int = 0, tokens: int = 2) -> torch.Tenso
     return torch.randn((1, tokens, cross_dim), generator=g, dtype=torch.float32)
 
 
-def synth_frames(n: int, h: int, w: int, seed: int = 0) -> torch.Tensor:
+def synth_frames(n: int, h: int, w: int, seed: int = 0, first: int = 0, count: int = None) -> torch.Tensor:
     """Synthetic video [n,3,h,w] in [-1,1]: smooth moving sinusoids + noise,
-    clipped to [0,1] then mapped as video_io.py:123."""
-    g = torch.Generator().manual_seed(seed)
-    u = torch.arange(w, dtype=torch.float32)[None, None, None, :] / w
-    v = torch.arange(h, dtype=torch.float32)[None, None, :, None] / h
-    k = torch.arange(n, dtype=torch.float32)[:, None, None, None] / max(n, 1)
-    f = torch.tensor([1.3, 2.1, 0.7], dtype=torch.float32)[None, :, None, None]
-    x = 0.5 + 0.35 * torch.sin(2 * math.pi * (u * f + v * (3.0 - f) + k * 1.5 + f))
-    x = x + 0.05 * torch.randn((n, 3, h, w), generator=g)
-    return x.clamp(0, 1) * 2.0 - 1.0
+    clipped to [0,1] then mapped as video_io.py:123.  `first`/`count` return frames
+    [first, first+count) of the same n-frame video (per-frame noise streams), so a rank can
+    materialise only its own chunk."""
+    count = n - first if count is None else count
+    u = torch.arange(w, dtype=torch.float32)[None, None, :] / w
+    v = torch.arange(h, dtype=torch.float32)[None, :, None] / h
+    f = torch.tensor([1.3, 2.1, 0.7], dtype=torch.float32)[:, None, None]
+    out = torch.empty((count, 3, h, w), dtype=torch.float32)
+    for i in range(count):
+        k = (first + i) / max(n, 1)
+        x = 0.5 + 0.35 * torch.sin(2 * math.pi * (u * f + v * (3.0 - f) + k * 1.5 + f))
+        g = torch.Generator().manual_seed(seed * 1000003 + first + i)
+        x = x + 0.05 * torch.randn((3, h, w), generator=g)
+        out[i] = x.clamp(0, 1) * 2.0 - 1.0
+    return out
 
 
 def synth_noise(h: int, w: int, seed: int = 1, c: int = 4) -> torch.Tensor:
