@@ -171,6 +171,20 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     _need(x, F16, "conv2d.x")
     _need(w, F16, "conv2d.w")
     B, H, W, Cin = x.shape
+    if B > 1 and B * H * W * Cin >= (1 << 30):  # 32-bit buffer offsets: split the batch
+        h = B // 2
+        Hi_, Wi_ = (2 * H, 2 * W) if upsample else (H, W)
+        if out_hw is None:
+            out_hw = ((Hi_ + 2 * pad - k) // stride + 1, (Wi_ + 2 * pad - k) // stride + 1)
+        if out is None:
+            out = torch.empty((B, out_hw[0], out_hw[1], cout), dtype=F16, device=x.device)
+        rb = rowbias if (rowbias is None or rowbias.dim() == 1) else None
+        for s0, s1 in ((0, h), (h, B)):
+            conv2d(x[s0:s1], w, cout, k, stride, pad, pad_tl, upsample, bias,
+                   None if residual is None else residual[s0:s1],
+                   rb if rb is not None or rowbias is None else rowbias[s0:s1],
+                   out[s0:s1], alpha, out_hw)
+        return out
     Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
     pt = pad if pad_tl is None else pad_tl
     if out_hw is None:
