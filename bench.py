@@ -111,7 +111,8 @@ def main():
 
     def step():
         if world > 1:
-            return sharded_forward(pipe, frames, list(dil0), True, 3, coalign, init_noise=noise, num_frames=N)
+            return sharded_forward(pipe, frames, list(dil0), True, 3, coalign, init_noise=noise, num_frames=N,
+                                   to_host=True)
         return pipe.forward(frames, list(dil0), True, [3], [1], [1], coalign, 0, 3, 6, None, False, 4, False,
                             init_noise=noise)
 

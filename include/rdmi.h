@@ -57,6 +57,10 @@ typedef struct rdmi_gemm_args {
   float alpha;
   int M, N, K, batch;
   int epilogue;
+  /* optional GroupNorm moments of the f16 output (batch == 1, f16 C, N % 4 == 0, M % 32 == 0):
+   * gn_part[v * gn_ld + 2*r + {0,1}] = (Σ, Σ²) over output rows 32r..32r+31 and channels
+   * 4v..4v+3, summed in a fixed order (rdmi_groupnorm_stats_partials consumes them).  NULL: off. */
+  float* gn_part; long gn_ld;
 } rdmi_gemm_args;
 int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
 
@@ -65,7 +69,10 @@ int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
  * y[b, ho, wo, co] = alpha * Σ w[co, dy, dx, ci] x[b, ho*s - pt + dy, wo*s - pl + dx, ci]
  *                    (+ bias[co]) (+ rowbias[b * rowbias_ld + co]) (+ residual[b, ho, wo, co])
  * `upsample`=1 reads x through a nearest ×2 upsample (Upsample2D, upsampling.py:141-190) without
- * materialising it.  Cin % 8 == 0 (pad channels); w is [Cout][kh][kw][Cin] padded to Kp % 32 == 0.
+ * materialising it.  Cin % 8 == 0 (pad channels).  Weight layout, zero padded to Kp % 32 == 0:
+ *   kh*kw > 1 and Cin % 32 == 0: [Cout][Cin/32][kh][kw][32] (channel-block major: the taps of one
+ *     32-channel block are adjacent in K, so the implicit-im2col re-reads of a block hit L2);
+ *   otherwise:                    [Cout][kh][kw][Cin].
  * Replaces the cuDNN conv2d of ResnetBlock2D.conv1/conv2/conv_shortcut (resnet.py:320-373),
  * Downsample2D (downsampling.py:132-148, including the VAE's F.pad(0,1,0,1) via pad_top/left=0
  * with the extra row/column read as zero), Upsample2D.conv, conv_in/conv_out of the UNet and VAE.
@@ -75,6 +82,7 @@ typedef struct rdmi_conv_args {
   const float* bias; const void* residual; const float* rowbias;
   int B, H, W, Cin, Cout, kh, kw, stride, pad_top, pad_left, upsample, Ho, Wo, Kp;
   long y_ld; long res_ld; float alpha; long rowbias_ld; /* 0: one row shared by all images */
+  float* gn_part; long gn_ld; /* GroupNorm moments of y, laid out as in rdmi_gemm_args; rows = B·Ho·Wo */
 } rdmi_conv_args;
 int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
 
@@ -88,6 +96,11 @@ int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
 long rdmi_groupnorm_workspace(int B, int G);
 int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G, float eps,
                          float* mean_rstd, float* workspace, void* stream);
+/* Statistics from the 32-row × 4-channel moments a producing GEMM/conv emitted (gn_part): for
+ * image b (rows b·HW .. b·HW+HW-1, HW % 32 == 0) and group g ((C/G) % 4 == 0), an f64 sum over the
+ * group's partials in a fixed order — independent of how many images share the tensor. */
+int rdmi_groupnorm_stats_partials(const float* part, long part_ld, int B, long HW, int C, int G, float eps,
+                                  float* mean_rstd, void* stream);
 int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G,
                          const float* mean_rstd, const float* gamma, const float* beta, int silu,
                          void* stream);

@@ -28,6 +28,7 @@ class GemmArgs(C.Structure):
         ("alpha", f32),
         ("M", i32), ("N", i32), ("K", i32), ("batch", i32),
         ("epilogue", i32),
+        ("gn_part", vp), ("gn_ld", i64),
     ]
 
 
@@ -39,6 +40,7 @@ class ConvArgs(C.Structure):
         ("stride", i32), ("pad_top", i32), ("pad_left", i32), ("upsample", i32), ("Ho", i32), ("Wo", i32),
         ("Kp", i32),
         ("y_ld", i64), ("res_ld", i64), ("alpha", f32), ("rowbias_ld", i64),
+        ("gn_part", vp), ("gn_ld", i64),
     ]
 
 
@@ -63,6 +65,7 @@ _SIGS = {
     "rdmi_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
     "rdmi_groupnorm_workspace": (i64, [i32, i32]),
     "rdmi_groupnorm_stats": (i32, [vp, i32, i64, i32, i32, f32, vp, vp, vp]),
+    "rdmi_groupnorm_stats_partials": (i32, [vp, i64, i32, i64, i32, i32, f32, vp, vp]),
     "rdmi_groupnorm_apply": (i32, [vp, vp, i32, i64, i32, i32, vp, vp, vp, i32, vp]),
     "rdmi_layernorm": (i32, [vp, vp, i64, i32, vp, vp, f32, vp]),
     "rdmi_attention_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i64, i64, i64,

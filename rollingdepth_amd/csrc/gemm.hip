@@ -27,6 +27,8 @@ struct GemmP {
   unsigned a_bytes, w_bytes;  // operand extents for the buffer descriptors (OOB lanes read 0)
   // convolution (A gathered from NHWC x)
   int IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
+  int cmaj;  // weights / K order channel-block major (rdmi.h): K-tile = one tap of 32 channels
+  float* gnp; long gn_ld;  // GroupNorm moments of the output (32 rows x 4 channels), or null
 };
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
@@ -39,6 +41,148 @@ constexpr unsigned OOB = 0x80000000u;  // byte offset past every descriptor's ex
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f16* l) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, 0, 0, 0);
+}
+
+// Epilogue shared by both engines.  The MFMA ran as Dᵀ = W·Aᵀ, so a lane holds 4 CONSECUTIVE
+// output channels n = fq*4 + r of one row m = lane&15: bias / time-embedding / residual are read
+// and the result written as 4-element vectors (8-B f16 / 16-B f32), scalar only at a ragged N
+// tail.  mw/nw: the wave's first output row / column.
+template <int RM, int RN, int WTN>
+__device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], int mw, int nw, int bz, int fr, int fq) {
+  const long cb = (long)bz * p.sC;
+  const long rbz = (long)bz * p.sR;
+  if (!p.geglu) {
+    static_assert(RM % 2 == 0, "GroupNorm moments pair 16-row tiles into 32-row blocks");
+    float gs[RN], gq[RN];  // per column tile: moments of this lane's 4 outputs over a 32-row block
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int m = mw + i * 16 + fr;
+      const bool mok = m < p.M;
+      const float* rbrow = p.rowbias && mok ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
+      const long crow = cb + (long)m * p.ldc;
+      const long rrow = rbz + (long)m * p.ldr;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = nw + j * 16 + fq * 4;
+        const bool ok = mok && n < p.N;
+        float s = 0.f, q = 0.f;
+        if (ok) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
+          if (p.vec && n + 3 < p.N) {
+            if (p.bias) {
+              const f32x4 bb = *(const f32x4*)(p.bias + n);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += bb[r];
+            }
+            if (rbrow) {
+              const f32x4 bb = *(const f32x4*)(rbrow + n);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += bb[r];
+            }
+            if (p.R) {
+              const f16x4 rr = *(const f16x4*)(p.R + rrow + n);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
+            }
+            if (p.silu) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
+            }
+            if (p.c_f32) {
+              *(f32x4*)((float*)p.C + crow + n) = f32x4{v[0], v[1], v[2], v[3]};
+            } else {
+              f16x4 o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+              *(f16x4*)((f16*)p.C + crow + n) = o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float f = (float)o[r];
+                s += f;
+                q = fmaf(f, f, q);
+              }
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int nn = n + r;
+              if (nn >= p.N) break;
+              float x = v[r];
+              if (p.bias) x += p.bias[nn];
+              if (rbrow) x += rbrow[nn];
+              if (p.R) x += (float)p.R[rrow + nn];
+              if (p.silu) x = silu_f(x);
+              if (p.c_f32)
+                ((float*)p.C)[crow + nn] = x;
+              else
+                ((f16*)p.C)[crow + nn] = (f16)x;
+            }
+          }
+        }
+        if (p.gnp) {  // host guarantees f16 output, N % 4 == 0, M % 32 == 0 (blocks whole)
+          if (!(i & 1)) {
+            gs[j] = s;
+            gq[j] = q;
+          } else {
+            s += gs[j];
+            q += gq[j];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) {  // fixed butterfly over the 16 rows of the tile
+              s += __shfl_xor(s, o, 64);
+              q += __shfl_xor(q, o, 64);
+            }
+            if (fr == 0 && ok) {
+              float* d = p.gnp + (long)(n >> 2) * p.gn_ld + (long)((m - 16) >> 5) * 2;
+              d[0] = s;
+              d[1] = q;
+            }
+          }
+        }
+      }
+    }
+  } else {
+    // GEGLU: within each wave's WTN(=64)-column slab, columns [0,32) are the value half and
+    // [32,64) the gate half of output columns slab*32 + [0,32) (N % 128 == 0: always vector).
+    static_assert(WTN == 64, "GEGLU slabs are 64 columns");
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int m = mw + i * 16 + fr;
+      if (m >= p.M) continue;
+      const long crow = cb + (long)m * p.ldc;
+#pragma unroll
+      for (int j = 0; j < RN / 2; ++j) {
+        const int nh = nw + j * 16 + fq * 4;
+        const int ng = nh + WTN / 2;
+        const int no = nw / 2 + j * 16 + fq * 4;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float h = acc[i][j][r] * p.alpha + (p.bias ? p.bias[nh + r] : 0.f);
+          const float g = acc[i][j + RN / 2][r] * p.alpha + (p.bias ? p.bias[ng + r] : 0.f);
+          v[r] = h * gelu_erf(g);
+          if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
+        }
+        if (p.c_f32) {
+          *(f32x4*)((float*)p.C + crow + no) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          f16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
+          *(f16x4*)((f16*)p.C + crow + no) = o;
+        }
+      }
+    }
+  }
+}
+
+// XCD-aware remap (T1): dispatch id d runs on XCD d % 8; give each XCD a contiguous range of
+// logical tiles so the n-tiles sharing one A row-panel share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int total) {
+  if (total < 8) return bid;
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
 // MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x for a 3×3 conv
@@ -66,16 +210,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  // XCD-aware remap (T1): dispatch id d runs on XCD d % 8; give each XCD a contiguous range of
-  // logical tiles so the n-tiles sharing one A row-panel share that XCD's L2.
-  const int nbx = gridDim.x, nby = gridDim.y;
-  const int total = nbx * nby;
-  const int bid = blockIdx.y * nbx + blockIdx.x;
-  int logical = bid;
-  if (total >= 8) {
-    const int xcd = bid & 7, q = total >> 3, r = total & 7;
-    logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  }
+  const int nbx = gridDim.x;
+  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
   const int n0 = (logical % nbx) * BN;
   const int m0 = (logical / nbx) * BM;
   const int bz = blockIdx.z;
@@ -118,10 +254,18 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
     const int n = n0 + (i * NW + wid) * 8 + lrow;
     brow[i] = n < p.N ? n * (int)p.ldw : -1;
   }
+  // A chunk → (tap, channel vector).  Tap-major K: chunk g of the K-tile is g-th vector of
+  // [tap][Cin]; channel-block major: 32-channel half h = chunk>>2 of the K-tile is block
+  // (cb, tap) = divmod(2u + h, 9) and its vector cb*4 + (chunk&3).
   int tap = 0, cv = chunk;
   if (MODE != 0) {
-    tap = chunk / p.cin_vecs;
-    cv = chunk - tap * p.cin_vecs;
+    if (p.cmaj) {
+      tap = chunk >> 2;
+      cv = chunk & 3;
+    } else {
+      tap = chunk / p.cin_vecs;
+      cv = chunk - tap * p.cin_vecs;
+    }
   }
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
 
@@ -152,10 +296,18 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
           off = arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cv * 8;
         dma16(ra_, ok ? (unsigned)off * 2u : OOB, la + (i * NW + wid) * 8 * BK);
       }
-      cv += 8;
-      while (cv >= p.cin_vecs) {
-        cv -= p.cin_vecs;
-        ++tap;
+      if (p.cmaj) {
+        tap += 2;
+        if (tap >= 9) {
+          tap -= 9;
+          cv += 4;
+        }
+      } else {
+        cv += 8;
+        while (cv >= p.cin_vecs) {
+          cv -= p.cin_vecs;
+          ++tap;
+        }
       }
     }
 #pragma unroll
@@ -207,109 +359,257 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
   }
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  // epilogue.  The MFMA ran as Dᵀ = W·Aᵀ, so a lane holds 4 CONSECUTIVE output channels
-  // n = fq*4 + r of one row m = lane&15: bias / time-embedding / residual are read and the
-  // result written as 4-element vectors (8-B f16 / 16-B f32), scalar only at a ragged N tail.
-  const long cb = (long)bz * p.sC;
-  const long rbz = (long)bz * p.sR;
-  if (!p.geglu) {
+  store_tile<RM, RN, WTN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, bz, fr, fq);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ping-pong engine for the large launches (the VAE decoder convolutions, big Linear layers).
+// BM×BN tile (256×256 or 512×128), 8 waves, each wave a 128×64 output sub-tile (8×4 16×16
+// accumulators).  K advances in 32-wide K-tiles through a 4-slot LDS ring (4 × 32 KiB, or
+// 4 × 40 KiB at 512×128), filled by LDS-DMA.  Each K-tile is two phases of 16 MFMAs per wave
+// (phase 0: the B sub-tile + A rows 0-63 of the wave; phase 1: A rows 64-127).  The two wave
+// groups (waves 0-3 and 4-7: one wave per SIMD each) run one barrier apart, so on every SIMD one
+// wave issues its 16 MFMAs while the other issues its ds_reads, address arithmetic and LDS-DMA
+// for the next phase (guide §5 "256² 8-phase template": ping-pong, s_setprio around the MFMAs).
+//
+// Schedule, with LOAD(q) the load section of phase q (q = 2·u + h for K-tile u):
+//   LOAD(q), q odd : s_waitcnt vmcnt(LPS)  (this wave's DMA of K-tile (q+1)/2 landed), then the
+//                    A-operand DMA of K-tile (q+5)/2;
+//   LOAD(q), q even: the B-operand DMA of K-tile (q+4)/2;
+//   then the phase's ds_reads.
+// RAW: K-tile u is first read in LOAD(2u); every wave's wait for it sits in LOAD(2u-1), which
+// precedes a barrier that every reader of LOAD(2u) has passed.  WAR: K-tile u overwrites the slot
+// of K-tile u-4, last read in LOAD(2u-7) (its ds_reads retired before that wave's next barrier);
+// the first DMA into the slot is issued in LOAD(2u-5), two barriers later.  Past the last K-tile
+// the DMAs read zero chunks (out-of-range offsets) so the vmcnt arithmetic stays uniform.
+// LDS row images are 64 B (32 halves); 16-B chunk c of row r is stored at c ^ (((r>>2)&1)<<1),
+// which makes the 16×16×32 fragment reads conflict-free on the ds_read_b128 lane groups.
+// DBG (ablation builds only, RDMI_GEMM_DBG): bit0 no main-loop DMA, bit1 no barriers in the loop,
+// bit2 no ds_reads in the loop.  Results are garbage; timings isolate the skeleton's costs.
+template <int BM, int BN, int MODE, int DBG = 0>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
+  constexpr int BKP = 32;
+  constexpr int NW = 8;
+  constexpr int WM = BM / 128, WN = BN / 64;
+  static_assert(WM * WN == NW, "8 waves of 128x64");
+  constexpr int RM = 8, RN = 4;
+  constexpr int AV = BM / 16 / NW;  // DMA instructions (16 rows x 64 B) per wave per K-tile
+  constexpr int BV = BN / 16 / NW;
+  constexpr int LPS = AV + BV;
+  constexpr int SLOT = (BM + BN) * BKP;
+  __shared__ __attribute__((aligned(16))) f16 lds[4 * SLOT];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int grp = wid >> 2;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nbx = gridDim.x;
+  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+  const int n0 = (logical % nbx) * BN;
+  const int m0 = (logical / nbx) * BM;
+  const int bz = blockIdx.z;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)bz * p.sA), (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.Wt + (long)bz * p.sW), (short)0, (int)p.w_bytes, 0x00020000);
+
+  const int lrow = lane >> 2;                              // row within the 16-row DMA piece
+  const int chunk = (lane & 3) ^ (((lrow >> 2) & 1) << 1);  // logical 16-B chunk this lane fetches
+  int arow[AV], ahb[AV], awb[AV];
 #pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + fr;
-      if (m >= p.M) continue;
-      const float* rbrow = p.rowbias ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
-      const long crow = cb + (long)m * p.ldc;
-      const long rrow = rbz + (long)m * p.ldr;
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + fq * 4;
-        if (n >= p.N) continue;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
-        if (p.vec && n + 3 < p.N) {
-          if (p.bias) {
-            const f32x4 bb = *(const f32x4*)(p.bias + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += bb[r];
-          }
-          if (rbrow) {
-            const f32x4 bb = *(const f32x4*)(rbrow + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += bb[r];
-          }
-          if (p.R) {
-            const f16x4 rr = *(const f16x4*)(p.R + rrow + n);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
-          }
-          if (p.silu) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
-          }
-          if (p.c_f32) {
-            *(f32x4*)((float*)p.C + crow + n) = f32x4{v[0], v[1], v[2], v[3]};
-          } else {
-            f16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
-            *(f16x4*)((f16*)p.C + crow + n) = o;
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int nn = n + r;
-            if (nn >= p.N) break;
-            float x = v[r];
-            if (p.bias) x += p.bias[nn];
-            if (rbrow) x += rbrow[nn];
-            if (p.R) x += (float)p.R[rrow + nn];
-            if (p.silu) x = silu_f(x);
-            if (p.c_f32)
-              ((float*)p.C)[crow + nn] = x;
-            else
-              ((f16*)p.C)[crow + nn] = (f16)x;
-          }
-        }
-      }
-    }
-  } else {
-    // GEGLU: within each wave's WTN(=64)-column slab, columns [0,32) are the value half and
-    // [32,64) the gate half of output columns slab*32 + [0,32) (N % 128 == 0: always vector).
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + fr;
-      if (m >= p.M) continue;
-      const long crow = cb + (long)m * p.ldc;
-#pragma unroll
-      for (int j = 0; j < RN / 2; ++j) {
-        const int nh = n0 + wn * WTN + j * 16 + fq * 4;
-        const int ng = nh + WTN / 2;
-        const int no = (n0 + wn * WTN) / 2 + j * 16 + fq * 4;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float h = acc[i][j][r] * p.alpha + (p.bias ? p.bias[nh + r] : 0.f);
-          const float g = acc[i][j + RN / 2][r] * p.alpha + (p.bias ? p.bias[ng + r] : 0.f);
-          v[r] = h * gelu_erf(g);
-          if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
-        }
-        if (p.c_f32) {
-          *(f32x4*)((float*)p.C + crow + no) = f32x4{v[0], v[1], v[2], v[3]};
-        } else {
-          f16x4 o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (f16)v[r];
-          *(f16x4*)((f16*)p.C + crow + no) = o;
-        }
-      }
+  for (int i = 0; i < AV; ++i) {
+    const int m = m0 + (i * NW + wid) * 16 + lrow;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    if (MODE != 0) {
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int r = mm - b * hw;
+      const int ho = r / p.Wo;
+      const int wo = r - ho * p.Wo;
+      const int hb = ho * p.stride - p.pt;
+      ahb[i] = ok ? hb : -(1 << 28);
+      awb[i] = wo * p.stride - p.pl;
+      arow[i] = MODE == 1 ? (b * p.IH + hb) * p.IW * p.Cin + awb[i] * p.Cin : b * p.IH * p.IW * p.Cin;
+    } else {
+      ahb[i] = ok ? 0 : -1;
+      awb[i] = 0;
+      arow[i] = mm * (int)p.lda;
     }
   }
+  int brow[BV];
+#pragma unroll
+  for (int i = 0; i < BV; ++i) {
+    const int n = n0 + (i * NW + wid) * 16 + lrow;
+    brow[i] = n < p.N ? n * (int)p.ldw : -1;
+  }
+  // A K-tiles are issued in order 0, 1, 2, ...: (tap, cv) of this lane's chunk advance by 4 vectors
+  // A chunk → (tap, channel vector), as in gemm_kernel with one 32-channel block per K-tile
+  int tap = 0, cv = chunk;
+  if (MODE != 0 && !p.cmaj) {
+    tap = chunk / p.cin_vecs;
+    cv = chunk - tap * p.cin_vecs;
+  }
+  const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
+  int ua = 0;  // next A K-tile to issue
+
+  auto issueA = [&]() {
+    const int kk = ua * BKP + chunk * 8;
+    const bool kok = kk < p.Kvalid;
+    f16* la = lds + (ua & 3) * SLOT;
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        const bool ok = ahb[i] == 0 && kok;
+        dma16(ra_, ok ? (unsigned)(arow[i] + kk) * 2u : OOB, la + (i * NW + wid) * 16 * BKP);
+      }
+    } else {
+      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9 (3x3 kernels only)
+      const int dx = tap - 3 * dy;
+      const int tapoff = (dy * p.IW + dx) * p.Cin + cv * 8;
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        const int hi = ahb[i] + dy, wi = awb[i] + dx;
+        const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
+        int off;
+        if (MODE == 1)
+          off = arow[i] + tapoff;
+        else
+          off = arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cv * 8;
+        dma16(ra_, ok ? (unsigned)off * 2u : OOB, la + (i * NW + wid) * 16 * BKP);
+      }
+      if (p.cmaj) {
+        if (++tap == 9) {
+          tap = 0;
+          cv += 4;
+        }
+      } else {
+        cv += 4;
+        while (cv >= p.cin_vecs) {
+          cv -= p.cin_vecs;
+          ++tap;
+        }
+      }
+    }
+    ++ua;
+  };
+  auto issueB = [&](int u) {
+    const int kk = u * BKP + chunk * 8;
+    const bool kok = kk < p.Kvalid;
+    f16* lb = lds + (u & 3) * SLOT + BM * BKP;
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const bool ok = brow[i] >= 0 && kok;
+      dma16(rw_, ok ? (unsigned)(brow[i] + kk) * 2u : OOB, lb + (i * NW + wid) * 16 * BKP);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BKP - 1) / BKP;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int fsw = (fq ^ (((fr >> 2) & 1) << 1)) << 3;  // swizzled chunk offset of this lane's fragment row
+
+  // prologue = LOAD(-5) .. LOAD(-1)
+  issueA();
+  issueB(0);
+  issueA();
+  issueB(1);
+  wait_vmcnt<LPS>();  // K-tile 0 landed (this wave)
+  issueA();           // K-tile 2
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // K-tile 0 visible to every wave
+  if (grp == 1 && !(DBG & 2)) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+  asm volatile("" ::: "memory");
+
+  f16x8 af[4] = {}, bf[RN] = {};
+  for (int u = 0; u < nk; ++u) {
+    const f16* la = lds + (u & 3) * SLOT + (wm * 128 + fr) * BKP + fsw;
+    const f16* lb = lds + (u & 3) * SLOT + BM * BKP + (wn * 64 + fr) * BKP + fsw;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // ---- LOAD(2u + h)
+      if (h == 1) {
+        if (!(DBG & 1)) {
+          wait_vmcnt<LPS>();  // K-tile u+1 landed (this wave)
+          issueA();           // K-tile u+3
+        }
+      } else {
+        if (!(DBG & 1)) issueB(u + 2);
+        if (!(DBG & 4)) {
+#pragma unroll
+          for (int j = 0; j < RN; ++j) bf[j] = *(const f16x8*)(lb + j * 16 * BKP);
+        } else {
+#pragma unroll
+          for (int j = 0; j < RN; ++j) asm volatile("" : "+v"(bf[j]));
+        }
+      }
+      if (!(DBG & 4)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const f16x8*)(la + (h * 64 + i * 16) * BKP);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(af[i]));
+      }
+      asm volatile("" ::: "memory");
+      if (!(DBG & 2)) __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // ---- MFMA(2u + h)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[h * 4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("" ::: "memory");
+      if (!(DBG & 2)) __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (grp == 0 && !(DBG & 2)) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
+  wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
+
+  store_tile<RM, RN, 64>(p, acc, m0 + wm * 128, n0 + wn * 64, bz, fr, fq);
+}
+
+// Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
+// engine only, 2 = ping-pong engine for every N % 128 == 0 launch, unset/1 = by size.
+int pp_mode() {
+  const char* e = getenv("RDMI_GEMM_PP");
+  return e ? atoi(e) : 1;
 }
 
 template <int MODE>
 void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
+  const int pp = pp_mode();
   const long mt256 = (p.M + 255) / 256;
+  // measured (tools/kbench.py, MI355X): the 256x256 ping-pong tile wins from about four waves of
+  // tiles on; the 512x128 one loses to the classic 256x128 engine, so it runs only when forced
+  const long min_tiles = pp == 2 ? 0 : 1024;
+  if ((pp == 2 && p.N % 128 == 0) || (pp == 1 && p.N % 256 == 0)) {
+    if (p.N % 256 == 0 && mt256 * (p.N / 256) * batch >= min_tiles) {
+      dim3 g(p.N / 256, rdmi::div_up(p.M, 256), batch);
+      const char* dbg = MODE == 0 ? getenv("RDMI_GEMM_DBG") : nullptr;
+      switch (dbg ? atoi(dbg) : 0) {
+        case 1: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 1>), g, dim3(512), 0, s, p); return;
+        case 3: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 3>), g, dim3(512), 0, s, p); return;
+        case 5: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 5>), g, dim3(512), 0, s, p); return;
+        case 7: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 7>), g, dim3(512), 0, s, p); return;
+        default: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE>), g, dim3(512), 0, s, p); return;
+      }
+    }
+    if (pp == 2) {
+      dim3 g(p.N / 128, rdmi::div_up(p.M, 512), batch);
+      hipLaunchKernelGGL((gemm_pp_kernel<512, 128, MODE>), g, dim3(512), 0, s, p);
+      return;
+    }
+  }
   if (force128 || p.N % 128 == 0 || p.N > 512) {
     if (mt256 * ((p.N + 127) / 128) * batch >= 512) {  // enough tiles to fill the chip with 256-row tiles
       dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 256), batch);
@@ -370,6 +670,10 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.silu = a->epilogue == RDMI_EPI_SILU;
   p.vec = vec_ok(p);
   RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm: GEGLU output needs 4-element aligned rows");
+  p.gnp = a->gn_part; p.gn_ld = a->gn_ld;
+  RDMI_REQUIRE(!p.gnp || (a->batch == 1 && !p.c_f32 && !p.geglu && p.vec && a->N % 4 == 0 && a->M % 32 == 0 &&
+                          ((uintptr_t)p.gnp & 7) == 0 && p.gn_ld >= 2L * (a->M / 32)),
+               RDMI_E_ARG, "gemm: GroupNorm moments need batch 1, f16 vector output, N %% 4 == 0, M %% 32 == 0");
   p.a_bytes = (unsigned)(((long)(a->M - 1) * a->lda + a->K) * 2);
   p.w_bytes = (unsigned)(((long)(a->N - 1) * a->ldw + a->K) * 2);
   return launch(p, a->batch, (hipStream_t)stream, p.geglu, 0);
@@ -394,6 +698,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   p.IH = a->H; p.IW = a->W; p.Cin = a->Cin; p.Ho = a->Ho; p.Wo = a->Wo;
   p.kh = a->kh; p.kw = a->kw; p.stride = a->stride; p.pt = a->pad_top; p.pl = a->pad_left;
   p.up = a->upsample ? 1 : 0; p.cin_vecs = a->Cin / 8;
+  p.cmaj = a->kh * a->kw > 1 && a->Cin % 32 == 0;
   // a 1×1, stride-1, unpadded conv on NHWC is a dense GEMM over pixels (conv_shortcut, quant convs)
   const bool dense = a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad_top == 0 && a->pad_left == 0 && !a->upsample &&
                      a->Ho == a->H && a->Wo == a->W;
@@ -401,6 +706,10 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   RDMI_REQUIRE(dense || (a->kh == 3 && a->kw == 3), RDMI_E_UNSUPPORTED, "conv2d: only 3x3 and dense 1x1 kernels");
   RDMI_REQUIRE(!a->upsample || a->stride == 1, RDMI_E_UNSUPPORTED, "conv2d: upsample needs stride 1");
   p.vec = vec_ok(p);
+  p.gnp = a->gn_part; p.gn_ld = a->gn_ld;
+  RDMI_REQUIRE(!p.gnp || (p.vec && a->Cout % 4 == 0 && p.M % 32 == 0 && ((uintptr_t)p.gnp & 7) == 0 &&
+                          p.gn_ld >= 2L * (p.M / 32)),
+               RDMI_E_ARG, "conv2d: GroupNorm moments need vector output, Cout %% 4 == 0, B*Ho*Wo %% 32 == 0");
   p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 2);
   p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 2);
   return launch(p, 1, (hipStream_t)stream, false, dense ? 0 : (a->upsample ? 2 : 1));

@@ -9,7 +9,10 @@ namespace {
 constexpr int GN_THREADS = 256;
 constexpr int GN_MAX_SPLIT = 256;
 
-// partial[b][split][g][2] (double sums)
+// partial[b][split][g][2] (double sums).  A thread owns one 8-channel column and a row lane,
+// streams its rows with four independent 16-B loads in flight and accumulates in f32 (at most a
+// few hundred rows per thread); the per-group combination of the threads' sums is f64 in a fixed
+// order.
 __global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__ x, long HW, int C, int G,
                                                          int split, double* __restrict__ part) {
   const int CV = C >> 3;
@@ -19,13 +22,13 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__
   const int RL = CV >= GN_THREADS ? 1 : GN_THREADS / CV;
   const int ncol = (CV + GN_THREADS - 1) / GN_THREADS;  // ≤ 2 (C ≤ 4096)
   const int t = threadIdx.x;
-  __shared__ double red[GN_THREADS][2][8][2];  // [thread][colset][elem][sum,sumsq] = 64 KB
+  __shared__ float red[2][8][2][GN_THREADS];  // [colset][elem][sum,sumsq][thread] = 32 KB
   const int cpg = C / G;
   const f16* xb = x + (long)b * HW * C;
   for (int cs = 0; cs < 2; ++cs) {
-    double s[8], ss[8];
+    float s[8], ss[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.0;
+    for (int e = 0; e < 8; ++e) s[e] = ss[e] = 0.f;
     int cv, rl;
     bool active;
     if (CV >= GN_THREADS) {
@@ -38,20 +41,35 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__
       active = cs == 0 && rl < RL;
     }
     if (active) {
-      for (long r = r0 + rl; r < r1; r += RL) {
-        f16x8 v = *(const f16x8*)(xb + r * C + cv * 8);
+      const f16* xp = xb + cv * 8;
+      long r = r0 + rl;
+      for (; r + 3 * RL < r1; r += 4 * RL) {
+        f16x8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *(const f16x8*)(xp + (r + u * RL) * C);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)v[u][e];
+            s[e] += f;
+            ss[e] = fmaf(f, f, ss[e]);
+          }
+      }
+      for (; r < r1; r += RL) {
+        const f16x8 v = *(const f16x8*)(xp + r * C);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          double f = (double)(float)v[e];
+          const float f = (float)v[e];
           s[e] += f;
-          ss[e] += f * f;
+          ss[e] = fmaf(f, f, ss[e]);
         }
       }
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[t][cs][e][0] = s[e];
-      red[t][cs][e][1] = ss[e];
+      red[cs][e][0][t] = s[e];
+      red[cs][e][1][t] = ss[e];
     }
   }
   __syncthreads();
@@ -62,13 +80,13 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__
       int cvv = c >> 3, e = c & 7;
       if (CV >= GN_THREADS) {
         int tt = cvv % GN_THREADS, cs = cvv / GN_THREADS;
-        S += red[tt][cs][e][0];
-        SS += red[tt][cs][e][1];
+        S += red[cs][e][0][tt];
+        SS += red[cs][e][1][tt];
       } else {
         for (int rl = 0; rl < RL; ++rl) {
           int tt = rl * CV + cvv;
-          S += red[tt][0][e][0];
-          SS += red[tt][0][e][1];
+          S += red[0][e][0][tt];
+          SS += red[0][e][1][tt];
         }
       }
     }
@@ -94,6 +112,46 @@ __global__ void gn_finalize(const double* __restrict__ part, int B, int G, int s
   if (var < 0) var = 0;
   mean_rstd[2 * i] = (float)mean;
   mean_rstd[2 * i + 1] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// Statistics from producer-emitted 32-row × 4-channel moments: one workgroup per (group, image);
+// thread t sums entries t, t+256, … of the group's [vec][block] range in f64, then a fixed-order
+// tree reduction.  The per-image work (and so every rounding) does not depend on B.
+__global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict__ part, long ld, long HW, int C,
+                                                        int G, float eps, float* __restrict__ mean_rstd) {
+  const int g = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int cpg = C / G;
+  const int nv = cpg >> 2;
+  const long nb = HW >> 5;
+  const long total = nv * nb;
+  const float* base = part + (long)(g * nv) * ld + (long)b * nb * 2;
+  double S = 0.0, SS = 0.0;
+  for (long i = t; i < total; i += 256) {
+    const long v = i / nb, k = i - v * nb;
+    const float* e = base + v * ld + k * 2;
+    S += (double)e[0];
+    SS += (double)e[1];
+  }
+  __shared__ double rs[256], rq[256];
+  rs[t] = S;
+  rq[t] = SS;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      rs[t] += rs[t + o];
+      rq[t] += rq[t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double n = (double)HW * cpg;
+    const double mean = rs[0] / n;
+    double var = rq[0] / n - mean * mean;
+    if (var < 0) var = 0;
+    const int i = b * G + g;
+    mean_rstd[2 * i] = (float)mean;
+    mean_rstd[2 * i + 1] = (float)(1.0 / sqrt(var + (double)eps));
+  }
 }
 
 // Streaming apply: each thread owns one 8-channel column (its 16 scale/shift values stay in
@@ -197,9 +255,10 @@ __global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f1
 
 // Split count depends on HW only (not on B), so a sample's statistics are bitwise identical
 // however many samples share the launch (snippet batching invariance).
-int gn_split(int /*B*/, long HW) {
-  long s = (HW + 255) / 256;
-  if (s > 64) s = 64;
+int gn_split(int /*B*/, long HW, int C) {
+  long s = (HW * C + 131071) / 131072;  // ~128 K elements per workgroup
+  if (s > GN_MAX_SPLIT) s = GN_MAX_SPLIT;
+  if (s > HW) s = HW;
   if (s < 1) s = 1;
   return (int)s;
 }
@@ -215,7 +274,7 @@ extern "C" int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G,
                "groupnorm_stats: bad C=%d G=%d", C, G);
   RDMI_REQUIRE(((uintptr_t)workspace & 7) == 0, RDMI_E_ALIGN, "groupnorm_stats: workspace not 8-byte aligned");
   hipStream_t s = (hipStream_t)stream;
-  int split = gn_split(B, HW);
+  int split = gn_split(B, HW, C);
   double* part = (double*)workspace;
   hipLaunchKernelGGL(gn_partial, dim3(split, B), dim3(GN_THREADS), 0, s, (const f16*)x, HW, C, G, split, part);
   int rc = rdmi::check_launch("groupnorm_partial");
@@ -223,6 +282,17 @@ extern "C" int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G,
   hipLaunchKernelGGL(gn_finalize, dim3(rdmi::div_up(B * G, 256)), dim3(256), 0, s, part, B, G, split,
                      (double)HW * (C / G), eps, mean_rstd);
   return rdmi::check_launch("groupnorm_finalize");
+}
+
+extern "C" int rdmi_groupnorm_stats_partials(const float* part, long part_ld, int B, long HW, int C, int G,
+                                             float eps, float* mean_rstd, void* stream) {
+  RDMI_REQUIRE(part && mean_rstd, RDMI_E_ARG, "groupnorm_stats_partials: null pointer");
+  RDMI_REQUIRE(G > 0 && C % G == 0 && (C / G) % 4 == 0 && HW % 32 == 0 && B > 0 && part_ld >= (long)B * HW / 16,
+               RDMI_E_ARG, "groupnorm_stats_partials: needs (C/G) %% 4 == 0 and HW %% 32 == 0 (C=%d G=%d HW=%ld)", C, G,
+               HW);
+  hipLaunchKernelGGL(gn_from_partials, dim3(G, B), dim3(256), 0, (hipStream_t)stream, part, part_ld, HW, C, G, eps,
+                     mean_rstd);
+  return rdmi::check_launch("groupnorm_stats_partials");
 }
 
 extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G, const float* mean_rstd,

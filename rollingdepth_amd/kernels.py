@@ -102,12 +102,15 @@ def pad_channels(c: int) -> int:
 
 
 def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> torch.Tensor:
-    """[Cout, Cin, kh, kw] → f16 [Cout, Kp] laid out [Cout][kh][kw][Cin_pad] (implicit-GEMM K
-    order of gemm.hip), zero padded to Kp % 32 == 0."""
+    """[Cout, Cin, kh, kw] → f16 [Cout, Kp] in the implicit-GEMM K order of gemm.hip (rdmi.h):
+    [Cout][Cin_pad/32][kh][kw][32] when kh·kw > 1 and Cin_pad % 32 == 0, else [Cout][kh][kw][Cin_pad];
+    zero padded to Kp % 32 == 0."""
     co, ci, kh, kw = w.shape
     cp = cin_pad or pad_channels(ci)
     t = torch.zeros((co, kh, kw, cp), dtype=F32)
     t[..., :ci] = w.permute(0, 2, 3, 1).float()
+    if kh * kw > 1 and cp % 32 == 0:
+        t = t.reshape(co, kh, kw, cp // 32, 32).permute(0, 3, 1, 2, 4).contiguous()
     k = kh * kw * cp
     kp = (k + 31) // 32 * 32
     out = torch.zeros((co, kp), dtype=F16)
@@ -119,9 +122,12 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> torch.T
 def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
          bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
          rowbias: Optional[torch.Tensor] = None, rows_per_group: int = 0, alpha: float = 1.0,
-         geglu: bool = False, out_f32: bool = False, n: Optional[int] = None, silu: bool = False) -> torch.Tensor:
+         geglu: bool = False, out_f32: bool = False, n: Optional[int] = None, silu: bool = False,
+         gn: bool = False) -> torch.Tensor:
     """out[m, :] = alpha·a[m, :k] @ w[:, :k]ᵀ + bias (+ rowbias[m // rows_per_group]) (+ residual).
-    a: f16 [..., M, lda]; w: f16 [N, Kp]; batched over a leading dim when a is 3-D."""
+    a: f16 [..., M, lda]; w: f16 [N, Kp]; batched over a leading dim when a is 3-D.
+    gn=True: the epilogue also emits the GroupNorm moments of the output (see _gn_part), which a
+    following `groupnorm(out, ...)` consumes instead of re-reading the tensor."""
     _need(a, F16, "gemm.a")
     _need(w, F16, "gemm.w")
     batch = a.shape[0] if a.dim() == 3 else 1
@@ -134,9 +140,36 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     g = _gemm_args(a, w, out, bias, residual, rowbias, rows_per_group, alpha, M, N, k, batch, geglu, out_f32)
     if silu:
         g.epilogue = 2
+    part = _gn_part(out, M, N) if (gn and batch == 1 and not geglu and not out_f32) else None
+    if part is not None:
+        g.gn_part, g.gn_ld = part.data_ptr(), part.stride(0)
     with _Timed("implicit_gemm", 2.0 * M * N * k * batch):
         check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
+    _gn_attach(out, part)
     return out
+
+
+# GroupNorm moments emitted by a producing GEMM/conv: f32 [N/4, M/32, 2] = (Σ, Σ²) over 32 rows × 4
+# channels of the f16 output (rdmi.h gn_part), attached to the output tensor object; groupnorm()
+# of that same tensor object uses them (rdmi_groupnorm_stats_partials) instead of a stats pass.
+_GN_ATTR = "_rdmi_gn_part"
+
+
+def _gn_part(out: torch.Tensor, M: int, N: int) -> Optional[torch.Tensor]:
+    if M % 32 or N % 4 or out.stride(-1) != 1 or out.stride(-2) != N or not out.is_contiguous():
+        return None
+    return torch.empty((N // 4, M // 32, 2), dtype=F32, device=out.device)
+
+
+def _gn_attach(out: torch.Tensor, part: Optional[torch.Tensor]):
+    setattr(out, _GN_ATTR, part)
+
+
+def gn_view(t: torch.Tensor, shape) -> torch.Tensor:
+    """t.view(shape) keeping t's GroupNorm moments (same memory, same row order)."""
+    v = t.view(shape)
+    _gn_attach(v, getattr(t, _GN_ATTR, None))
+    return v
 
 
 def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, geglu, out_f32):
@@ -165,35 +198,37 @@ def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, 
 def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1, pad: int = 1,
            pad_tl: Optional[int] = None, upsample: bool = False, bias: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, rowbias: Optional[torch.Tensor] = None,
-           out: Optional[torch.Tensor] = None, alpha: float = 1.0, out_hw=None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, alpha: float = 1.0, out_hw=None, gn: bool = False,
+           _gn_slot=None) -> torch.Tensor:
     """NHWC f16 conv.  x [B, H, W, Cin_pad]; w packed by pack_conv.  `pad` is symmetric; pad_tl
-    overrides the top/left padding with bottom/right implied by out_hw (VAE Downsample2D)."""
+    overrides the top/left padding with bottom/right implied by out_hw (VAE Downsample2D).
+    gn=True: also emit the output's GroupNorm moments (as gemm)."""
     _need(x, F16, "conv2d.x")
     _need(w, F16, "conv2d.w")
     B, H, W, Cin = x.shape
-    if B > 1 and B * H * W * Cin >= (1 << 30):  # 32-bit buffer offsets: split the batch
-        h = B // 2
-        Hi_, Wi_ = (2 * H, 2 * W) if upsample else (H, W)
-        if out_hw is None:
-            out_hw = ((Hi_ + 2 * pad - k) // stride + 1, (Wi_ + 2 * pad - k) // stride + 1)
-        if out is None:
-            out = torch.empty((B, out_hw[0], out_hw[1], cout), dtype=F16, device=x.device)
-        rb = rowbias if (rowbias is None or rowbias.dim() == 1) else None
-        for s0, s1 in ((0, h), (h, B)):
-            conv2d(x[s0:s1], w, cout, k, stride, pad, pad_tl, upsample, bias,
-                   None if residual is None else residual[s0:s1],
-                   rb if rb is not None or rowbias is None else rowbias[s0:s1],
-                   out[s0:s1], alpha, out_hw)
-        return out
     Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
     pt = pad if pad_tl is None else pad_tl
     if out_hw is None:
-        Ho = (Hi + 2 * pad - k) // stride + 1
-        Wo = (Wi + 2 * pad - k) // stride + 1
-    else:
-        Ho, Wo = out_hw
+        out_hw = ((Hi + 2 * pad - k) // stride + 1, (Wi + 2 * pad - k) // stride + 1)
+    Ho, Wo = out_hw
     if out is None:
         out = torch.empty((B, Ho, Wo, cout), dtype=F16, device=x.device)
+    part = _gn_part(out, B * Ho * Wo, cout) if gn and _gn_slot is None else None
+    if B > 1 and B * H * W * Cin >= (1 << 30):  # 32-bit buffer offsets: split the batch
+        h = B // 2
+        rb = rowbias if (rowbias is None or rowbias.dim() == 1) else None
+        for s0, s1 in ((0, h), (h, B)):
+            slot = None
+            if part is not None and (s0 * Ho * Wo) % 32 == 0:
+                slot = (part.data_ptr() + (s0 * Ho * Wo // 32) * 2 * 4, part.stride(0))
+            elif part is not None:
+                part = None
+            conv2d(x[s0:s1], w, cout, k, stride, pad, pad_tl, upsample, bias,
+                   None if residual is None else residual[s0:s1],
+                   rb if rb is not None or rowbias is None else rowbias[s0:s1],
+                   out[s0:s1], alpha, out_hw, _gn_slot=slot)
+        _gn_attach(out, part)
+        return out
     a = _N.ConvArgs()
     a.x, a.w, a.y = x.data_ptr(), w.data_ptr(), out.data_ptr()
     a.bias, a.residual, a.rowbias = _p(bias), _p(residual), _p(rowbias)
@@ -206,8 +241,14 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     a.rowbias_ld = 0 if (rowbias is not None and rowbias.dim() == 1) else (rowbias.stride(0) if rowbias is not None else 0)
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
+    if part is not None:
+        a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
+    elif _gn_slot is not None:
+        a.gn_part, a.gn_ld = _gn_slot
     with _Timed("implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
+    if _gn_slot is None:
+        _gn_attach(out, part)
     return out
 
 
@@ -229,6 +270,11 @@ def groupnorm_stats(x: torch.Tensor, groups: int, eps: float) -> torch.Tensor:
     B, C = x.shape[0], x.shape[-1]
     HW = x.numel() // (B * C)
     mr = torch.empty((B * groups * 2,), dtype=F32, device=x.device)
+    part = getattr(x, _GN_ATTR, None)
+    if part is not None and HW % 32 == 0 and (C // groups) % 4 == 0 and part.shape == (C // 4, B * HW // 32, 2):
+        check(lib.rdmi_groupnorm_stats_partials(part.data_ptr(), part.stride(0), B, HW, C, groups, eps, mr.data_ptr(),
+                                                _stream()), "rdmi_groupnorm_stats_partials")
+        return mr
     ws = _workspace(lib.rdmi_groupnorm_workspace(B, groups), x.device)
     check(lib.rdmi_groupnorm_stats(x.data_ptr(), B, HW, C, groups, eps, mr.data_ptr(), ws.data_ptr(), _stream()),
           "rdmi_groupnorm_stats")
@@ -241,6 +287,7 @@ def groupnorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
     B, C = x.shape[0], x.shape[-1]
     HW = x.numel() // (B * C)
     out = torch.empty_like(x) if out is None else out
+    _gn_attach(out, None)
     check(lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), B, HW, C, groups, mr.data_ptr(), gamma.data_ptr(),
                                    beta.data_ptr(), int(silu), _stream()), "rdmi_groupnorm_apply")
     return out

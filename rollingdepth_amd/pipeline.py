@@ -153,6 +153,24 @@ class RollingDepthPipeline:
             dilation = min(max_gap, dilation)
         return dilation
 
+    # ------------------------------------------------------------------ host <-> device plumbing
+    def _device_index(self, values) -> torch.Tensor:
+        """int32 index list → device tensor through pinned memory, without a host sync (a plain
+        torch.tensor(..., device=) waits for the stream and drains the GPU's queue)."""
+        t = torch.tensor(values, dtype=torch.int32).pin_memory()
+        return t.to(self.device, non_blocking=True)
+
+    @staticmethod
+    def _to_host_async(t: torch.Tensor, stream) -> torch.Tensor:
+        """Enqueue a device→host copy into pinned memory on `stream` (after the work queued so far
+        on the current stream).  The result is valid once `stream` is synchronised."""
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        stream.wait_stream(torch.cuda.current_stream(t.device))
+        with torch.cuda.stream(stream):
+            h.copy_(t, non_blocking=True)
+        t.record_stream(stream)
+        return h
+
     # ------------------------------------------------------------------ stages
     def encode_rgb(self, frames_nchw: torch.Tensor) -> torch.Tensor:
         """[N,3,H,W] in [-1,1] (any float dtype, on device) → NHWC f16 [N, h, w, 8] latents·0.18215."""
@@ -197,9 +215,11 @@ class RollingDepthPipeline:
             idx = self.get_snippet_indice(0, timesteps, N, slen, dil, dil, stride)
             buf = torch.empty((len(idx), slen, H, W), dtype=F16, device=self.device)
             todo = list(range(len(idx))) if snippet_subset is None else list(snippet_subset[di])
+            fidx_all = self._device_index([f for s in todo for f in idx[s]]) if todo else None
+            pos_all = self._device_index(todo) if todo else None
             for b0 in range(0, len(todo), self.snippet_batch):
                 sel = todo[b0:b0 + self.snippet_batch]
-                fidx = torch.tensor([f for s in sel for f in idx[s]], dtype=torch.int32, device=self.device)
+                fidx = fidx_all[b0 * slen:(b0 + len(sel)) * slen]
                 x = K.gather_unet_input(rgb_latent, init_noise, fidx, depth_bcast=True)
                 depth_view = x[..., 4:8]
                 for si, t in enumerate(timesteps.tolist()):
@@ -226,7 +246,7 @@ class RollingDepthPipeline:
                     else dec.view(len(sel) * slen, H, W, 1)
                 self.decode_depth(zin, tgt)
                 if dec is None:
-                    buf[torch.tensor(sel, device=self.device)] = tgt.view(len(sel), slen, H, W)
+                    buf[pos_all[b0:b0 + len(sel)].long()] = tgt.view(len(sel), slen, H, W)
             outs.append(buf)
         return outs
 
@@ -249,9 +269,10 @@ class RollingDepthPipeline:
             idx = self.get_snippet_indice(i_step, ts, N, snippet_len, start_dilation, 1, 1)
             stride = idx[0][1] - idx[0][0] if snippet_len > 1 else 1
             preds = torch.empty((len(idx), snippet_len, h, w, 8), dtype=F16, device=self.device)
+            fidx_all = self._device_index([f for s in idx for f in s])
             for b0 in range(0, len(idx), self.snippet_batch):
                 sel = idx[b0:b0 + self.snippet_batch]
-                fidx = torch.tensor([f for s in sel for f in s], dtype=torch.int32, device=self.device)
+                fidx = fidx_all[b0 * snippet_len:(b0 + len(sel)) * snippet_len]
                 x = K.gather_unet_input(rgb_latent, new, fidx, depth_bcast=False)
                 pred = self.unet.forward(x, int(t), num_view=snippet_len)
                 self.scheduler.step_(pred, int(t), x[..., 4:8], 1.0, channels=4,
@@ -326,9 +347,12 @@ class RollingDepthPipeline:
         noise = K.nchw_to_nhwc(init_noise.to(self.device), 8)
         snippets = self.init_snippet_infer(rgb_latent, noise, dilations, snippet_lengths, init_infer_steps, strides,
                                            record=record)
+        # snippet_ls D2H (the reference returns it on the host) overlaps the aligner's kernels
+        H, W = snippets[0].shape[-2:]
+        d2h = torch.cuda.Stream(self.device)
+        snip_host = [self._to_host_async(s.view(s.shape[0], s.shape[1], 1, H, W), d2h) for s in snippets]
         # ----------------- co-alignment + renormalisation (:306-318)
         aligner = DepthAligner(device=self.device, verbose=verbose, **(coalign_kwargs or {}))
-        H, W = snippets[0].shape[-2:]
         merged, scales, trans, hist = aligner.run([s.view(s.shape[0], s.shape[1], 1, H, W) for s in snippets],
                                                   dilations)
         d = merged.float().contiguous()
@@ -349,7 +373,11 @@ class RollingDepthPipeline:
             depth = dec.view(N, 1, H, W)
         else:
             depth = coaligned
-        # ----------------- outputs (:345-353, D2H boundary)
-        snip_out = [s.view(s.shape[0], s.shape[1], 1, H, W).cpu() for s in snippets]
-        return RollingDepthOutput(input_rgb=input_frames[0].float().cpu() / 2.0 + 0.5, depth_pred=depth.cpu(),
-                                  snippet_ls=snip_out, depth_coaligned=coaligned.cpu())
+        # ----------------- outputs (:345-353, D2H boundary; pinned, async, one sync)
+        # input_rgb = frames / 2 + 0.5 in f16 as the reference computes it on the host (x/2 is exact,
+        # the +0.5 rounds identically), evaluated on the device before the copy
+        rgb = input_frames[0].to(self.device, F16) / 2.0 + 0.5
+        outs = [self._to_host_async(t, d2h) for t in (rgb, depth, coaligned)]
+        d2h.synchronize()
+        return RollingDepthOutput(input_rgb=outs[0], depth_pred=outs[1], snippet_ls=snip_host,
+                                  depth_coaligned=outs[2])

@@ -76,13 +76,18 @@ def gather_snippets(local: torch.Tensor, counts: Sequence[int], world: int, grou
 @torch.no_grad()
 def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool = True,
                     snippet_len: int = 3, coalign_kwargs=None, init_noise: torch.Tensor = None, group=None,
-                    num_frames: int = None):
+                    num_frames: int = None, to_host: bool = False):
     """Multi-GPU RollingDepthPipeline.forward (refine_step = 0).  Returns the depth [N,1,H,W] f16
     on rank 0 (None elsewhere) and the per-dilation snippets on rank 0.
 
     `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N`
     — only this rank's contiguous chunk chunk_bounds(N, world)[rank] (each rank then holds 1/W of
-    the video in host/device memory)."""
+    the video in host/device memory).
+
+    `to_host=True` mirrors forward()'s D2H boundary, distributed: every rank copies its own chunk
+    of input_rgb and its own snippet rows to pinned host memory (overlapping the gathers and the
+    aligner), rank 0 the coaligned depth; rank 0 returns (depth_host, per-dilation device
+    snippets), other ranks (None, None) — after their copies completed."""
     from . import kernels as K
     from .aligner import DepthAligner
 
@@ -117,12 +122,26 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     snippets = pipe.init_snippet_infer(rgb_latent, noise, dil, [snippet_len] * len(dil), [1] * len(dil),
                                        [1] * len(dil), snippet_subset=subsets)
     local = local_rows(snippets, counts, world, rank)
+    d2h = torch.cuda.Stream(dev) if to_host else None
+    if to_host:
+        for t in local:
+            if t.shape[0]:
+                pipe._to_host_async(t, d2h)
+        if hi > lo:
+            pipe._to_host_async(mine_frames.to(dev, F16) / 2.0 + 0.5, d2h)
     # 3. all-gather decoded snippets, co-align on rank 0
     per_d = gather_snippets(local, counts, world, group)
     if rank != 0:
+        if d2h is not None:
+            d2h.synchronize()
         return None, None
     aligner = DepthAligner(device=dev, **(coalign_kwargs or {}))
     merged, _, _, _ = aligner.run([s.view(s.shape[0], snippet_len, 1, H, W) for s in per_d], dil)
     d = merged.float().contiguous()
     K.renormalize_(d, K.minmax(d))
-    return d.to(F16), per_d
+    depth = d.to(F16)
+    if d2h is not None:
+        depth = pipe._to_host_async(depth, d2h)
+        pipe._to_host_async(d.to(F16), d2h)  # depth_pred (== coaligned without refine)
+        d2h.synchronize()
+    return depth, per_d

@@ -45,8 +45,8 @@ class _Lin:
         self.w = K.pack_linear(w, dev)
         self.b = sd[key + ".bias"].to(dev, F32) if bias and key + ".bias" in sd else None
 
-    def __call__(self, x, out=None, residual=None, silu=False):
-        return K.gemm(x, self.w, self.k, out=out, bias=self.b, residual=residual, silu=silu)
+    def __call__(self, x, out=None, residual=None, silu=False, gn=False):
+        return K.gemm(x, self.w, self.k, out=out, bias=self.b, residual=residual, silu=silu, gn=gn)
 
 
 class _Conv:
@@ -58,9 +58,11 @@ class _Conv:
         self.b = sd[key + ".bias"].to(dev, F32) if key + ".bias" in sd else None
         self.stride, self.pad = stride, pad
 
-    def __call__(self, x, upsample=False, residual=None, rowbias=None, out=None, pad_tl=None, out_hw=None):
+    def __call__(self, x, upsample=False, residual=None, rowbias=None, out=None, pad_tl=None, out_hw=None, gn=False):
+        """gn=True when a GroupNorm consumes the output (its moments come from this epilogue)."""
         return K.conv2d(x, self.w, self.cout, self.k, stride=self.stride, pad=self.pad, pad_tl=pad_tl,
-                        upsample=upsample, bias=self.b, residual=residual, rowbias=rowbias, out=out, out_hw=out_hw)
+                        upsample=upsample, bias=self.b, residual=residual, rowbias=rowbias, out=out, out_hw=out_hw,
+                        gn=gn)
 
 
 class _Norm:
@@ -87,10 +89,10 @@ class Resnet:
         if self.temb_slot is not None and temb_all is not None:
             o, w = self.temb_slot
             rb = temb_all[o:o + w]
-        h = self.c1(h, rowbias=rb)
+        h = self.c1(h, rowbias=rb, gn=True)
         h = K.groupnorm(h, self.n2.g, self.n2.b, self.groups, self.eps, silu=True)
         res = self.sc(x) if self.sc is not None else x
-        return self.c2(h, residual=res)
+        return self.c2(h, residual=res, gn=True)
 
 
 class Transformer:
@@ -154,8 +156,8 @@ class Transformer:
         n3 = K.layernorm(t, self.ln3.g, self.ln3.b, 1e-5)
         f = K.gemm(n3, self.ff1_w, C, bias=self.ff1_b, geglu=True)
         t = self.ff2(f, residual=t)
-        out = self.proj_out(t, residual=x.view(B * HW, C))
-        return out.view(B, H, W, C)
+        out = self.proj_out(t, residual=x.view(B * HW, C), gn=True)
+        return K.gn_view(out, (B, H, W, C))
 
 
 class UNet:
@@ -251,7 +253,7 @@ class UNet:
         if h % f or w % f:
             raise NotImplementedError(f"latent {h}x{w} not a multiple of {f} (forward_upsample_size path)")
         temb = self.time_embedding(t)
-        x = self.conv_in(sample)
+        x = self.conv_in(sample, gn=True)
         skips = [x]
         for blk in self.down:
             for j, r in enumerate(blk["res"]):
@@ -260,7 +262,7 @@ class UNet:
                     x = blk["attn"][j](x, num_view)
                 skips.append(x)
             if blk["ds"] is not None:
-                x = blk["ds"](x)
+                x = blk["ds"](x, gn=True)
                 skips.append(x)
         x = self.mid_res[0](x, temb)
         x = self.mid_attn(x, num_view)
@@ -272,6 +274,6 @@ class UNet:
                 if blk["attn"]:
                     x = blk["attn"][j](x, num_view)
             if blk["us"] is not None:
-                x = blk["us"](x, upsample=True)
+                x = blk["us"](x, upsample=True, gn=True)
         x = K.groupnorm(x, self.norm_out.g, self.norm_out.b, self.groups, self.eps, silu=True)
         return self.conv_out(x)

@@ -58,8 +58,8 @@ class VaeAttention:
         del s
         vt = K.transpose(v)
         o = K.gemm(p, vt, S)
-        out = self.out(o.view(B * S, C), residual=x.view(B * S, C))
-        return out.view(B, H, W, C)
+        out = self.out(o.view(B * S, C), residual=x.view(B * S, C), gn=True)
+        return K.gn_view(out, (B, H, W, C))
 
 
 class VAE:
@@ -119,13 +119,13 @@ class VAE:
         B, H, W, _ = x.shape
         if H % self.factor or W % self.factor:
             raise NotImplementedError(f"frame {H}x{W} not a multiple of {self.factor}")
-        h = self.e_in(x)
+        h = self.e_in(x, gn=True)
         for res, ds in self.e_down:
             for r in res:
                 h = r(h)
             if ds is not None:
                 # Downsample2D(padding=0): F.pad(0,1,0,1) then 3×3 s2 (downsampling.py:141-146)
-                h = ds(h, pad_tl=0, out_hw=(h.shape[1] // 2, h.shape[2] // 2))
+                h = ds(h, pad_tl=0, out_hw=(h.shape[1] // 2, h.shape[2] // 2), gn=True)
         h = self.e_mid[0](h)
         h = self.e_attn(h)
         h = self.e_mid[1](h)
@@ -142,7 +142,7 @@ class VAE:
         B, hh, ww, _ = z.shape
         h = torch.zeros((B, hh, ww, self.d_in.cin_pad), dtype=F16, device=z.device)
         self.post_quant(z, out=h)
-        h = self.d_in(h)
+        h = self.d_in(h, gn=True)
         h = self.d_mid[0](h)
         h = self.d_attn(h)
         h = self.d_mid[1](h)
@@ -150,6 +150,6 @@ class VAE:
             for r in res:
                 h = r(h)
             if us is not None:
-                h = us(h, upsample=True)
+                h = us(h, upsample=True, gn=True)
         h = K.groupnorm(h, self.d_norm.g, self.d_norm.b, self.groups, 1e-6, silu=True)
         return self.d_out(h, out=out)

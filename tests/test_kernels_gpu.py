@@ -18,13 +18,22 @@ def _k():
     return K
 
 
+@pytest.fixture(params=["auto", "classic", "pingpong"])
+def engine(request, monkeypatch):
+    """GEMM/conv engine: by size (auto), the 3-slot classic engine only, or the ping-pong engine
+    forced for every N % 128 == 0 launch (RDMI_GEMM_PP, gemm.hip)."""
+    monkeypatch.setenv("RDMI_GEMM_PP", {"auto": "1", "classic": "0", "pingpong": "2"}[request.param])
+    return request.param
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 320, 320), (1000, 960, 320), (77, 64, 1024), (5, 1280, 320),
-                                   (513, 200, 40)])
-def test_gemm_bias_residual(M, N, K):
+                                   (513, 200, 40), (1000, 256, 320), (700, 128, 1024), (1300, 512, 40),
+                                   (33, 384, 96), (600, 640, 2880)])
+def test_gemm_bias_residual(M, N, K, engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(0)
     a = torch.randn(M, K, device=DEV, generator=g).half()
@@ -37,7 +46,7 @@ def test_gemm_bias_residual(M, N, K):
     assert _rel(y, ref) < 4e-3
 
 
-def test_gemm_rowbias_alpha_f32out_batched():
+def test_gemm_rowbias_alpha_f32out_batched(engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(1)
     B, M, N, K = 3, 200, 256, 96
@@ -54,7 +63,7 @@ def test_gemm_rowbias_alpha_f32out_batched():
     assert _rel(y2, ref2) < 4e-3
 
 
-def test_gemm_geglu():
+def test_gemm_geglu(engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(2)
     M, C = 333, 320
@@ -72,8 +81,10 @@ def test_gemm_geglu():
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,stride,pad,up", [
     (2, 16, 16, 320, 320, 3, 1, 1, False), (1, 24, 20, 8, 320, 3, 1, 1, False), (2, 12, 12, 128, 128, 3, 2, 1, False),
     (1, 9, 7, 64, 64, 3, 1, 1, True), (2, 10, 10, 3, 32, 3, 1, 1, False), (1, 8, 8, 64, 4, 3, 1, 1, False),
-    (2, 11, 13, 40, 24, 1, 1, 0, False)])
-def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up):
+    (2, 11, 13, 40, 24, 1, 1, 0, False), (2, 20, 18, 256, 256, 3, 1, 1, False), (1, 17, 15, 128, 128, 3, 1, 1, True),
+    (2, 14, 14, 8, 128, 3, 1, 1, False), (1, 13, 11, 320, 640, 3, 2, 1, False), (2, 9, 10, 512, 512, 3, 1, 1, True),
+    (1, 12, 12, 40, 256, 3, 1, 1, False)])
+def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(3)
     x = torch.randn(B, Cin, H, W, device=DEV, generator=g).half()
@@ -87,7 +98,7 @@ def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up):
     assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
 
 
-def test_conv2d_vae_downsample_rowbias_residual():
+def test_conv2d_vae_downsample_rowbias_residual(engine):
     """Downsample2D with padding=0: F.pad(0,1,0,1) then 3x3 s2 (downsampling.py:141-146)."""
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(4)
@@ -120,6 +131,51 @@ def test_groupnorm(C, G, HW, silu, eps):
     if silu:
         ref = F.silu(ref)
     assert (y.float() - ref).abs().max().item() < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,up", [(2, 16, 16, 64, 128, False), (3, 12, 12, 128, 256, True),
+                                                (1, 24, 20, 256, 512, False)])
+def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine):
+    """Conv epilogue-emitted GroupNorm moments (rdmi.h gn_part) vs the standalone stats pass and an
+    fp32 reference; the moments of each image are bitwise independent of the batch they ran in."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(B, H, W, Cin, device=DEV, generator=g).half()
+    w = K_.pack_conv(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), DEV)
+    res = torch.randn(B, 2 * H if up else H, 2 * W if up else W, Cout, device=DEV, generator=g).half()
+    y = K_.conv2d(x, w, Cout, 3, upsample=up, residual=res, gn=True)
+    assert getattr(y, K_._GN_ATTR) is not None
+    mr_fused = K_.groupnorm_stats(y, 32, 1e-6)
+    y_plain = y.clone()  # no moments attached: standalone stats pass
+    mr_plain = K_.groupnorm_stats(y_plain, 32, 1e-6)
+    HW = y.shape[1] * y.shape[2]
+    yf = y.float().view(B, HW, 32, Cout // 32)
+    mean = yf.mean(dim=(1, 3)).flatten()
+    rstd = (yf.var(dim=(1, 3), unbiased=False).flatten() + 1e-6).rsqrt()
+    assert torch.allclose(mr_fused.view(-1, 2)[:, 0], mean, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(mr_fused.view(-1, 2)[:, 1], rstd, rtol=1e-4)
+    assert torch.allclose(mr_fused, mr_plain, rtol=1e-5, atol=1e-6)
+    # batch invariance: image 0 alone
+    y0 = K_.conv2d(x[:1], w, Cout, 3, upsample=up, residual=res[:1], gn=True)
+    assert torch.equal(y0, y[:1])
+    mr0 = K_.groupnorm_stats(y0, 32, 1e-6)
+    assert torch.equal(mr0, mr_fused[: mr0.numel()])
+
+
+def test_groupnorm_moments_from_gemm(engine):
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(12)
+    B, HW, C = 2, 576, 512
+    a = torch.randn(B * HW, 256, device=DEV, generator=g).half()
+    w = K_.pack_linear(torch.randn(C, 256, device=DEV, generator=g) / 16, DEV)
+    r = torch.randn(B * HW, C, device=DEV, generator=g).half()
+    y = K_.gemm(a, w, 256, residual=r, gn=True)
+    yv = K_.gn_view(y, (B, 24, 24, C))
+    gm = torch.ones(C, device=DEV)
+    bt = torch.zeros(C, device=DEV)
+    out = K_.groupnorm(yv, gm, bt, 32, 1e-6, True)
+    ref = F.silu(F.group_norm(yv.float().permute(0, 3, 1, 2), 32, gm, bt, 1e-6)).permute(0, 2, 3, 1)
+    assert (out.float() - ref).abs().max().item() < 1e-2
 
 
 @pytest.mark.parametrize("C", [320, 640, 1280])

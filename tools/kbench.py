@@ -68,6 +68,50 @@ def bench_gemm(iters):
         print(f"gemm  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
 
+def bench_square(iters):
+    """Dense square GEMMs: the engine against a plain-GEMM yardstick (guide §5 256² template)."""
+    for n in (4096, 8192):
+        a = (torch.rand(n, n, device="cuda") * 2 - 1).half()
+        w = (torch.rand(n, n, device="cuda") * 2 - 1).half()
+        out = torch.empty(n, n, device="cuda", dtype=torch.float16)
+        ms = timeit(lambda: K.gemm(a, w, n, out=out), iters)
+        print(f"gemm  square {n}^3{'':22s} {ms * 1e3:9.1f} us  {2.0 * n ** 3 / ms / 1e9:8.1f} TFLOP/s")
+        ms = timeit(lambda: torch.matmul(a, w.t(), out=out), iters)
+        print(f"torch square {n}^3{'':22s} {ms * 1e3:9.1f} us  {2.0 * n ** 3 / ms / 1e9:8.1f} TFLOP/s")
+
+
+def bench_shapes(iters):
+    """Dense GEMM scaling probe over M, N, K (fixed-overhead vs K-loop rate)."""
+    print("CUs:", torch.cuda.get_device_properties(0).multi_processor_count)
+    for m, n, k in [(4096, 4096, 4096), (4096, 4096, 8192), (4096, 4096, 16384), (8192, 4096, 4096),
+                    (16384, 4096, 4096), (8192, 8192, 4096), (8192, 8192, 8192)]:
+        a = (torch.rand(m, k, device="cuda") * 2 - 1).half()
+        w = (torch.rand(n, k, device="cuda") * 2 - 1).half()
+        out = torch.empty(m, n, device="cuda", dtype=torch.float16)
+        ms = timeit(lambda: K.gemm(a, w, k, out=out), iters)
+        print(f"gemm  {m}x{n}x{k}{'':18s} {ms * 1e3:9.1f} us  {2.0 * m * n * k / ms / 1e9:8.1f} TFLOP/s")
+
+
+def bench_host(iters):
+    """Host-side cost of one wrapper call (tiny problem: the GPU finishes first)."""
+    import time
+    a = torch.randn(16, 64, device="cuda").half()
+    w = K.pack_linear(torch.randn(128, 64), "cuda")
+    x = torch.randn(1, 8, 8, 64, device="cuda").half()
+    wc = K.pack_conv(torch.randn(64, 64, 3, 3), "cuda")
+    for lab, fn in (("gemm", lambda: K.gemm(a, w, 64)), ("conv2d", lambda: K.conv2d(x, wc, 64, 3)),
+                    ("empty launch", lambda: torch.empty(1, device="cuda").zero_())):
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(200):
+            fn()
+        dt = (time.perf_counter() - t0) / 200
+        torch.cuda.synchronize()
+        print(f"host  {lab:32s} {dt * 1e6:9.1f} us per call")
+
+
 def bench_attn(iters):
     for lab, B, S, H in [("L0 S=27648 H=5 b=8", 8, 27648, 5), ("L1 S=6912 H=10 b=8", 8, 6912, 10),
                          ("L2 S=1728 H=20 b=8", 8, 1728, 20), ("mid S=432 H=20 b=8", 8, 432, 20)]:
@@ -104,4 +148,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn}[part](a.iters)
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
