@@ -70,8 +70,9 @@ int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
  *                    (+ bias[co]) (+ rowbias[b * rowbias_ld + co]) (+ residual[b, ho, wo, co])
  * `upsample`=1 reads x through a nearest ×2 upsample (Upsample2D, upsampling.py:141-190) without
  * materialising it.  Cin % 8 == 0 (pad channels).  Weight layout, zero padded to Kp % 32 == 0:
- *   kh*kw > 1 and Cin % 32 == 0: [Cout][Cin/32][kh][kw][32] (channel-block major: the taps of one
- *     32-channel block are adjacent in K, so the implicit-im2col re-reads of a block hit L2);
+ *   kh*kw > 1 and Cin % 64 == 0: [Cout][Cin/64][kh][kw][64] (channel-block major: one K-tile of 64
+ *     is one tap of a 64-channel block, i.e. one full 128-B line per output pixel, and the taps of
+ *     a block are adjacent in K, so the implicit-im2col re-reads of a block hit L2);
  *   otherwise:                    [Cout][kh][kw][Cin].
  * Replaces the cuDNN conv2d of ResnetBlock2D.conv1/conv2/conv_shortcut (resnet.py:320-373),
  * Downsample2D (downsampling.py:132-148, including the VAE's F.pad(0,1,0,1) via pad_top/left=0

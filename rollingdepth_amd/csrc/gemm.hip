@@ -27,8 +27,9 @@ struct GemmP {
   unsigned a_bytes, w_bytes;  // operand extents for the buffer descriptors (OOB lanes read 0)
   // convolution (A gathered from NHWC x)
   int IH, IW, Cin, Ho, Wo, kh, kw, stride, pt, pl, up, cin_vecs;
-  int cmaj;  // weights / K order channel-block major (rdmi.h): K-tile = one tap of 32 channels
+  int cmaj;  // weights / K order channel-block major (rdmi.h): K-tile = one tap of 64 channels
   float* gnp; long gn_ld;  // GroupNorm moments of the output (32 rows x 4 channels), or null
+  int group_m;  // tile order inside an XCD's range: groups of group_m m-tiles, n-tiles within a group
 };
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
@@ -185,6 +186,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// logical tile → (m-tile, n-tile): groups of G m-tiles sweep all n-tiles with m fastest, so the
+// tiles an XCD runs together share G A-panels and a few B-panels (L2 reuse in both operands)
+__device__ __forceinline__ void tile_mn(int logical, int nbx, int nby, int G, int& mt, int& nt) {
+  if (G <= 1) {
+    mt = logical / nbx;
+    nt = logical % nbx;
+    return;
+  }
+  const int per = G * nbx;
+  const int g = logical / per;
+  const int first = g * G;
+  const int gs = min(G, nby - first);
+  const int r = logical - g * per;
+  mt = first + r % gs;
+  nt = r / gs;
+}
+
 // MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x for a 3×3 conv
 // (any stride/padding); MODE 2: 3×3 conv reading x through a nearest ×2 upsample.
 // Operands reach LDS by LDS-DMA (buffer_load_dwordx4 … lds: no VGPR staging, no ds_write) into a
@@ -212,8 +230,10 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
   const int wm = wid / WN, wn = wid % WN;
   const int nbx = gridDim.x;
   const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
-  const int n0 = (logical % nbx) * BN;
-  const int m0 = (logical / nbx) * BM;
+  int mt_, nt_;
+  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN;
+  const int m0 = mt_ * BM;
   const int bz = blockIdx.z;
   const __amdgpu_buffer_rsrc_t ra_ =
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)bz * p.sA), (short)0, (int)p.a_bytes, 0x00020000);
@@ -259,9 +279,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
   // (cb, tap) = divmod(2u + h, 9) and its vector cb*4 + (chunk&3).
   int tap = 0, cv = chunk;
   if (MODE != 0) {
-    if (p.cmaj) {
-      tap = chunk >> 2;
-      cv = chunk & 3;
+    if (p.cmaj) {  // K-tile u = tap u % 9 of the 64-channel block u / 9
+      tap = 0;
+      cv = chunk;
     } else {
       tap = chunk / p.cin_vecs;
       cv = chunk - tap * p.cin_vecs;
@@ -297,10 +317,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
         dma16(ra_, ok ? (unsigned)off * 2u : OOB, la + (i * NW + wid) * 8 * BK);
       }
       if (p.cmaj) {
-        tap += 2;
-        if (tap >= 9) {
-          tap -= 9;
-          cv += 4;
+        if (++tap == 9) {
+          tap = 0;
+          cv += 8;
         }
       } else {
         cv += 8;
@@ -363,145 +382,138 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Ping-pong engine for the large launches (the VAE decoder convolutions, big Linear layers).
-// BM×BN tile (256×256 or 512×128), 8 waves, each wave a 128×64 output sub-tile (8×4 16×16
-// accumulators).  K advances in 32-wide K-tiles through a 4-slot LDS ring (4 × 32 KiB, or
-// 4 × 40 KiB at 512×128), filled by LDS-DMA.  Each K-tile is two phases of 16 MFMAs per wave
-// (phase 0: the B sub-tile + A rows 0-63 of the wave; phase 1: A rows 64-127).  The two wave
-// groups (waves 0-3 and 4-7: one wave per SIMD each) run one barrier apart, so on every SIMD one
-// wave issues its 16 MFMAs while the other issues its ds_reads, address arithmetic and LDS-DMA
-// for the next phase (guide §5 "256² 8-phase template": ping-pong, s_setprio around the MFMAs).
-//
-// Schedule, with LOAD(q) the load section of phase q (q = 2·u + h for K-tile u):
-//   LOAD(q), q odd : s_waitcnt vmcnt(LPS)  (this wave's DMA of K-tile (q+1)/2 landed), then the
-//                    A-operand DMA of K-tile (q+5)/2;
-//   LOAD(q), q even: the B-operand DMA of K-tile (q+4)/2;
-//   then the phase's ds_reads.
-// RAW: K-tile u is first read in LOAD(2u); every wave's wait for it sits in LOAD(2u-1), which
-// precedes a barrier that every reader of LOAD(2u) has passed.  WAR: K-tile u overwrites the slot
-// of K-tile u-4, last read in LOAD(2u-7) (its ds_reads retired before that wave's next barrier);
-// the first DMA into the slot is issued in LOAD(2u-5), two barriers later.  Past the last K-tile
-// the DMAs read zero chunks (out-of-range offsets) so the vmcnt arithmetic stays uniform.
-// LDS row images are 64 B (32 halves); 16-B chunk c of row r is stored at c ^ (((r>>2)&1)<<1),
-// which makes the 16×16×32 fragment reads conflict-free on the ds_read_b128 lane groups.
+// Ping-pong engine for the large launches (the VAE / UNet convolutions, big Linear layers).
+// 256×256 tile, 8 waves (2 M × 4 N), each wave a 128×64 output sub-tile (8×4 16×16 f32
+// accumulators).  K advances in 64-wide K-tiles (one full 128-B line per operand row) through a
+// 2-slot LDS ring (2 × 64 KiB) filled by LDS-DMA.  Each K-tile is four phases of 16 MFMAs per
+// wave:  p0 = (A rows 0-63 of the wave, k 0-31), p1 = (rows 0-63, k 32-63), p2 = (rows 64-127,
+// k 0-31), p3 = (rows 64-127, k 32-63); the B fragments of both k halves are read in p0/p1 and
+// stay in registers for p2/p3.  The two wave groups (waves 0-3 and 4-7: one wave per SIMD each)
+// run one barrier apart, so on every SIMD one wave issues its 16 MFMAs while the other issues its
+// ds_reads, address arithmetic and LDS-DMA for a later K-tile (guide §5 "256² 8-phase template":
+// ping-pong, s_setprio around the MFMAs, counted vmcnt, raw s_barrier).
+// Every load section first issues its fragment reads, then 2 DMA instructions per wave (8 per
+// K-tile: B halves B0/B1, A halves A0 = rows 0-63, A1 = rows 64-127 of each wave row), 3-5 phases
+// ahead of their first read:
+//   LOAD(4u)   : A0(u+1)          LOAD(4u+1): wait A1(u) (vmcnt 6), A1(u+1)
+//   LOAD(4u+2) : B0(u+2)          LOAD(4u+3): wait B(u+1), A0(u+1) (vmcnt 4), B1(u+2)
+// with LOAD(q) the load section of phase q = 4·(K-tile) + p.  RAW: each wave's wait sits in the
+// load section before the first read of the data, which is followed by a barrier that every
+// reader (either group) passes first.  WAR: B(u) and A0(u) are last read in LOAD(4u+1), which ends
+// with s_waitcnt lgkmcnt(0) before its barrier, so B(u)'s region is free from the next phase on in
+// either group (the groups are one barrier apart): B0(u+2) lands there in LOAD(4u+2), B1(u+2) in
+// LOAD(4u+3), A0(u+2) in LOAD(4u+4); A1(u+2) overwrites A1(u), last read in LOAD(4u+3), in
+// LOAD(4u+5).  Past the last K-tile the DMAs read zero chunks (out-of-range offsets) so the vmcnt
+// arithmetic stays uniform.
+// LDS row images are 128 B (64 halves); 16-B chunk c of row r is stored at c ^ (r & 7) (source
+// side of the DMA, guide rule 21), which makes the 16×16×32 fragment reads conflict-free on the
+// ds_read_b128 lane groups, and lets every 8-lane group of a DMA read one whole 128-B line.
+// Conv (MODE 1/2) needs the channel-block-major K order with 64-channel blocks (p.cmaj): K-tile u
+// is tap u % 9 of channels 64·(u / 9) .. +63.
 // DBG (ablation builds only, RDMI_GEMM_DBG): bit0 no main-loop DMA, bit1 no barriers in the loop,
-// bit2 no ds_reads in the loop.  Results are garbage; timings isolate the skeleton's costs.
-template <int BM, int BN, int MODE, int DBG = 0>
+// bit2 no ds_reads in the loop, bit3 no MFMAs.  Results are garbage; timings isolate the skeleton's costs.
+template <int MODE, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
-  constexpr int BKP = 32;
-  constexpr int NW = 8;
-  constexpr int WM = BM / 128, WN = BN / 64;
-  static_assert(WM * WN == NW, "8 waves of 128x64");
+  constexpr int BM = 256, BN = 256, BKP = 64;
   constexpr int RM = 8, RN = 4;
-  constexpr int AV = BM / 16 / NW;  // DMA instructions (16 rows x 64 B) per wave per K-tile
-  constexpr int BV = BN / 16 / NW;
-  constexpr int LPS = AV + BV;
-  constexpr int SLOT = (BM + BN) * BKP;
-  __shared__ __attribute__((aligned(16))) f16 lds[4 * SLOT];
+  constexpr int SLOT = (BM + BN) * BKP;  // halves (64 KiB)
+  __shared__ __attribute__((aligned(16))) f16 lds[2 * SLOT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int grp = wid >> 2;
-  const int wm = wid / WN, wn = wid % WN;
+  const int wm = wid >> 2, wn = wid & 3;
   const int nbx = gridDim.x;
   const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
-  const int n0 = (logical % nbx) * BN;
-  const int m0 = (logical / nbx) * BM;
+  int mt_, nt_;
+  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN;
+  const int m0 = mt_ * BM;
   const int bz = blockIdx.z;
   const __amdgpu_buffer_rsrc_t ra_ =
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)bz * p.sA), (short)0, (int)p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw_ =
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.Wt + (long)bz * p.sW), (short)0, (int)p.w_bytes, 0x00020000);
 
-  const int lrow = lane >> 2;                              // row within the 16-row DMA piece
-  const int chunk = (lane & 3) ^ (((lrow >> 2) & 1) << 1);  // logical 16-B chunk this lane fetches
-  int arow[AV], ahb[AV], awb[AV];
+  // DMA lane geometry: one 1-KiB instruction = 8 rows × 128 B; lane → (row lrow, phys chunk lane&7)
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ lrow;  // logical chunk fetched (row & 7 == lrow: piece rows start at multiples of 8)
+  // A pieces of this wave: half h, e = 0/1 → tile rows (t>>3)*128 + h*64 + (t&7)*8, t = wid + 8e
+  int arow[2][2], ahb[2][2], awb[2][2];
 #pragma unroll
-  for (int i = 0; i < AV; ++i) {
-    const int m = m0 + (i * NW + wid) * 16 + lrow;
-    const bool ok = m < p.M;
-    const int mm = ok ? m : 0;
-    if (MODE != 0) {
-      const int hw = p.Ho * p.Wo;
-      const int b = mm / hw;
-      const int r = mm - b * hw;
-      const int ho = r / p.Wo;
-      const int wo = r - ho * p.Wo;
-      const int hb = ho * p.stride - p.pt;
-      ahb[i] = ok ? hb : -(1 << 28);
-      awb[i] = wo * p.stride - p.pl;
-      arow[i] = MODE == 1 ? (b * p.IH + hb) * p.IW * p.Cin + awb[i] * p.Cin : b * p.IH * p.IW * p.Cin;
-    } else {
-      ahb[i] = ok ? 0 : -1;
-      awb[i] = 0;
-      arow[i] = mm * (int)p.lda;
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int t = wid + 8 * e;
+      const int m = m0 + (t >> 3) * 128 + h * 64 + (t & 7) * 8 + lrow;
+      const bool ok = m < p.M;
+      const int mm = ok ? m : 0;
+      if (MODE != 0) {
+        const int hw = p.Ho * p.Wo;
+        const int b = mm / hw;
+        const int r = mm - b * hw;
+        const int ho = r / p.Wo;
+        const int wo = r - ho * p.Wo;
+        const int hb = ho * p.stride - p.pt;
+        ahb[h][e] = ok ? hb : -(1 << 28);
+        awb[h][e] = wo * p.stride - p.pl;
+        arow[h][e] = MODE == 1 ? (b * p.IH + hb) * p.IW * p.Cin + awb[h][e] * p.Cin : b * p.IH * p.IW * p.Cin;
+      } else {
+        ahb[h][e] = ok ? 0 : -1;
+        awb[h][e] = 0;
+        arow[h][e] = mm * (int)p.lda;
+      }
     }
-  }
-  int brow[BV];
+  int brow[4];
 #pragma unroll
-  for (int i = 0; i < BV; ++i) {
-    const int n = n0 + (i * NW + wid) * 16 + lrow;
-    brow[i] = n < p.N ? n * (int)p.ldw : -1;
-  }
-  // A K-tiles are issued in order 0, 1, 2, ...: (tap, cv) of this lane's chunk advance by 4 vectors
-  // A chunk → (tap, channel vector), as in gemm_kernel with one 32-channel block per K-tile
-  int tap = 0, cv = chunk;
-  if (MODE != 0 && !p.cmaj) {
-    tap = chunk / p.cin_vecs;
-    cv = chunk - tap * p.cin_vecs;
+  for (int e = 0; e < 4; ++e) {
+    const int n = n0 + (wid + 8 * e) * 8 + lrow;
+    brow[e] = n < p.N ? n * (int)p.ldw : -1;
   }
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
-  int ua = 0;  // next A K-tile to issue
 
-  auto issueA = [&]() {
-    const int kk = ua * BKP + chunk * 8;
-    const bool kok = kk < p.Kvalid;
-    f16* la = lds + (ua & 3) * SLOT;
+  auto issueA = [&](int h, int u) {
+    f16* la = lds + (u & 1) * SLOT;
     if (MODE == 0) {
+      const int kk = u * BKP + chunk * 8;
+      const bool kok = kk < p.Kvalid;
 #pragma unroll
-      for (int i = 0; i < AV; ++i) {
-        const bool ok = ahb[i] == 0 && kok;
-        dma16(ra_, ok ? (unsigned)(arow[i] + kk) * 2u : OOB, la + (i * NW + wid) * 16 * BKP);
+      for (int e = 0; e < 2; ++e) {
+        const int t = wid + 8 * e;
+        const bool ok = ahb[h][e] == 0 && kok;
+        dma16(ra_, ok ? (unsigned)(arow[h][e] + kk) * 2u : OOB,
+              la + ((t >> 3) * 128 + h * 64 + (t & 7) * 8) * BKP);
       }
     } else {
-      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9 (3x3 kernels only)
-      const int dx = tap - 3 * dy;
-      const int tapoff = (dy * p.IW + dx) * p.Cin + cv * 8;
+      const int cb = u / 9;  // wave-uniform
+      const int tap = u - cb * 9;
+      const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+      const bool kok = cb * 64 < p.Cin;
+      const int cofs = cb * 64 + chunk * 8;
+      const int tapoff = (dy * p.IW + dx) * p.Cin + cofs;
 #pragma unroll
-      for (int i = 0; i < AV; ++i) {
-        const int hi = ahb[i] + dy, wi = awb[i] + dx;
+      for (int e = 0; e < 2; ++e) {
+        const int t = wid + 8 * e;
+        const int hi = ahb[h][e] + dy, wi = awb[h][e] + dx;
         const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
         int off;
         if (MODE == 1)
-          off = arow[i] + tapoff;
+          off = arow[h][e] + tapoff;
         else
-          off = arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cv * 8;
-        dma16(ra_, ok ? (unsigned)off * 2u : OOB, la + (i * NW + wid) * 16 * BKP);
-      }
-      if (p.cmaj) {
-        if (++tap == 9) {
-          tap = 0;
-          cv += 4;
-        }
-      } else {
-        cv += 4;
-        while (cv >= p.cin_vecs) {
-          cv -= p.cin_vecs;
-          ++tap;
-        }
+          off = arow[h][e] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cofs;
+        dma16(ra_, ok ? (unsigned)off * 2u : OOB, la + ((t >> 3) * 128 + h * 64 + (t & 7) * 8) * BKP);
       }
     }
-    ++ua;
   };
-  auto issueB = [&](int u) {
+  auto issueB = [&](int hb, int u) {  // B pieces e = 2hb, 2hb+1 of K-tile u
     const int kk = u * BKP + chunk * 8;
     const bool kok = kk < p.Kvalid;
-    f16* lb = lds + (u & 3) * SLOT + BM * BKP;
+    f16* lb = lds + (u & 1) * SLOT + BM * BKP;
 #pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      const bool ok = brow[i] >= 0 && kok;
-      dma16(rw_, ok ? (unsigned)(brow[i] + kk) * 2u : OOB, lb + (i * NW + wid) * 16 * BKP);
+    for (int e = 2 * hb; e < 2 * hb + 2; ++e) {
+      const bool ok = brow[e] >= 0 && kok;
+      dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 8 * e) * 8 * BKP);
     }
   };
 
@@ -513,59 +525,79 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 
   const int nk = (p.K + BKP - 1) / BKP;
   const int fr = lane & 15, fq = lane >> 4;
-  const int fsw = (fq ^ (((fr >> 2) & 1) << 1)) << 3;  // swizzled chunk offset of this lane's fragment row
+  // fragment offsets (halves) of this lane's row fr for the two k halves: chunk (4kh + fq) ^ (fr & 7)
+  const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
+  const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
 
-  // prologue = LOAD(-5) .. LOAD(-1)
-  issueA();
-  issueB(0);
-  issueA();
-  issueB(1);
-  wait_vmcnt<LPS>();  // K-tile 0 landed (this wave)
-  issueA();           // K-tile 2
+  // prologue: K-tile 0 whole, B of K-tile 1; wait for B(0) + A0(0)
+  issueB(0, 0);
+  issueB(1, 0);
+  issueA(0, 0);
+  issueA(1, 0);
+  issueB(0, 1);
+  issueB(1, 1);
+  wait_vmcnt<6>();
   asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // K-tile 0 visible to every wave
+  __builtin_amdgcn_s_barrier();  // K-tile 0 (B, A first half) visible to every wave
   if (grp == 1 && !(DBG & 2)) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   asm volatile("" ::: "memory");
 
-  f16x8 af[4] = {}, bf[RN] = {};
+  f16x8 af[4] = {}, bf[2][RN] = {};
   for (int u = 0; u < nk; ++u) {
-    const f16* la = lds + (u & 3) * SLOT + (wm * 128 + fr) * BKP + fsw;
-    const f16* lb = lds + (u & 3) * SLOT + BM * BKP + (wn * 64 + fr) * BKP + fsw;
+    const f16* la = lds + (u & 1) * SLOT + (wm * 128) * BKP;
+    const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * 64) * BKP;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      // ---- LOAD(2u + h)
-      if (h == 1) {
-        if (!(DBG & 1)) {
-          wait_vmcnt<LPS>();  // K-tile u+1 landed (this wave)
-          issueA();           // K-tile u+3
-        }
-      } else {
-        if (!(DBG & 1)) issueB(u + 2);
-        if (!(DBG & 4)) {
-#pragma unroll
-          for (int j = 0; j < RN; ++j) bf[j] = *(const f16x8*)(lb + j * 16 * BKP);
-        } else {
-#pragma unroll
-          for (int j = 0; j < RN; ++j) asm volatile("" : "+v"(bf[j]));
-        }
-      }
+    for (int ph = 0; ph < 4; ++ph) {
+      const int h = ph >> 1, kh = ph & 1;
+      // ---- LOAD(4u + ph): this phase's fragment reads first (their latency hides under the DMA
+      // issue that follows), then the waits / DMA for later K-tiles
       if (!(DBG & 4)) {
+        const int off = kh ? off1 : off0;
+        if (h == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = *(const f16x8*)(la + (h * 64 + i * 16) * BKP);
+          for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const f16x8*)(la + (h * 64 + i * 16) * BKP + off);
       } else {
+#pragma unroll
+        for (int j = 0; j < RN; ++j) asm volatile("" : "+v"(bf[kh][j]));
 #pragma unroll
         for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(af[i]));
       }
+      if (!(DBG & 1)) {
+        if (ph == 0) {
+          issueA(0, u + 1);
+        } else if (ph == 1) {
+          wait_vmcnt<6>();  // A1(u) landed (B(u+1), A0(u+1) in flight)
+          issueA(1, u + 1);
+        } else if (ph == 2) {
+          issueB(0, u + 2);
+        } else {
+          wait_vmcnt<4>();  // B(u+1), A0(u+1) landed (A1(u+1), B0(u+2) in flight)
+          issueB(1, u + 2);
+        }
+      }
+      // the last reads of B and A0 (p1) retire before the barrier: B0(u+2) re-fills B(u)'s region
+      // in the next load section (either group)
+      if (ph == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       asm volatile("" ::: "memory");
       if (!(DBG & 2)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      // ---- MFMA(2u + h)
+      // ---- MFMA(4u + ph)
       __builtin_amdgcn_s_setprio(1);
+      if (!(DBG & 8)) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[h * 4 + i][j], 0, 0, 0);
+          for (int j = 0; j < RN; ++j)
+            acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[i], acc[h * 4 + i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i]));
+#pragma unroll
+        for (int j = 0; j < RN; ++j) asm volatile("" ::"v"(bf[kh][j]));
+      }
       __builtin_amdgcn_s_setprio(0);
       asm volatile("" ::: "memory");
       if (!(DBG & 2)) __builtin_amdgcn_s_barrier();
@@ -577,6 +609,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 
   store_tile<RM, RN, 64>(p, acc, m0 + wm * 128, n0 + wn * 64, bz, fr, fq);
 }
+
 
 // Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
 // engine only, 2 = ping-pong engine for every N % 128 == 0 launch, unset/1 = by size.
@@ -590,24 +623,17 @@ void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
   const int pp = pp_mode();
   const long mt256 = (p.M + 255) / 256;
   // measured (tools/kbench.py, MI355X): the 256x256 ping-pong tile wins from about four waves of
-  // tiles on; the 512x128 one loses to the classic 256x128 engine, so it runs only when forced
+  // tiles on (RDMI_GEMM_PP=2: whenever the shape allows it)
   const long min_tiles = pp == 2 ? 0 : 1024;
-  if ((pp == 2 && p.N % 128 == 0) || (pp == 1 && p.N % 256 == 0)) {
-    if (p.N % 256 == 0 && mt256 * (p.N / 256) * batch >= min_tiles) {
-      dim3 g(p.N / 256, rdmi::div_up(p.M, 256), batch);
-      const char* dbg = MODE == 0 ? getenv("RDMI_GEMM_DBG") : nullptr;
-      switch (dbg ? atoi(dbg) : 0) {
-        case 1: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 1>), g, dim3(512), 0, s, p); return;
-        case 3: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 3>), g, dim3(512), 0, s, p); return;
-        case 5: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 5>), g, dim3(512), 0, s, p); return;
-        case 7: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE, 7>), g, dim3(512), 0, s, p); return;
-        default: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, MODE>), g, dim3(512), 0, s, p); return;
-      }
-    }
-    if (pp == 2) {
-      dim3 g(p.N / 128, rdmi::div_up(p.M, 512), batch);
-      hipLaunchKernelGGL((gemm_pp_kernel<512, 128, MODE>), g, dim3(512), 0, s, p);
-      return;
+  if (pp != 0 && p.N % 256 == 0 && (MODE == 0 || p.cmaj) && mt256 * (p.N / 256) * batch >= min_tiles) {
+    dim3 g(p.N / 256, rdmi::div_up(p.M, 256), batch);
+    const char* dbg = MODE == 0 ? getenv("RDMI_GEMM_DBG") : nullptr;
+    switch (dbg ? atoi(dbg) : 0) {
+      case 1: hipLaunchKernelGGL((gemm_pp_kernel<0, 1>), g, dim3(512), 0, s, p); return;
+      case 5: hipLaunchKernelGGL((gemm_pp_kernel<0, 5>), g, dim3(512), 0, s, p); return;
+      case 8: hipLaunchKernelGGL((gemm_pp_kernel<0, 8>), g, dim3(512), 0, s, p); return;
+      case 12: hipLaunchKernelGGL((gemm_pp_kernel<0, 12>), g, dim3(512), 0, s, p); return;
+      default: hipLaunchKernelGGL((gemm_pp_kernel<MODE>), g, dim3(512), 0, s, p); return;
     }
   }
   if (force128 || p.N % 128 == 0 || p.N > 512) {
@@ -624,7 +650,9 @@ void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
   }
 }
 
-int launch(const GemmP& p, int batch, hipStream_t s, bool force128, int mode) {
+int launch(GemmP p, int batch, hipStream_t s, bool force128, int mode) {
+  const char* gm = getenv("RDMI_GEMM_GROUP");
+  p.group_m = gm ? atoi(gm) : 8;  // measured: 8 m-tiles per group (tools/abl.sh, 8192³: +7 %)
   if (mode == 2)
     launch_mode<2>(p, batch, s, force128);
   else if (mode == 1)
@@ -698,7 +726,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   p.IH = a->H; p.IW = a->W; p.Cin = a->Cin; p.Ho = a->Ho; p.Wo = a->Wo;
   p.kh = a->kh; p.kw = a->kw; p.stride = a->stride; p.pt = a->pad_top; p.pl = a->pad_left;
   p.up = a->upsample ? 1 : 0; p.cin_vecs = a->Cin / 8;
-  p.cmaj = a->kh * a->kw > 1 && a->Cin % 32 == 0;
+  p.cmaj = a->kh * a->kw > 1 && a->Cin % 64 == 0;
   // a 1×1, stride-1, unpadded conv on NHWC is a dense GEMM over pixels (conv_shortcut, quant convs)
   const bool dense = a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad_top == 0 && a->pad_left == 0 && !a->upsample &&
                      a->Ho == a->H && a->Wo == a->W;

@@ -103,14 +103,14 @@ def pad_channels(c: int) -> int:
 
 def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> torch.Tensor:
     """[Cout, Cin, kh, kw] → f16 [Cout, Kp] in the implicit-GEMM K order of gemm.hip (rdmi.h):
-    [Cout][Cin_pad/32][kh][kw][32] when kh·kw > 1 and Cin_pad % 32 == 0, else [Cout][kh][kw][Cin_pad];
+    [Cout][Cin_pad/64][kh][kw][64] when kh·kw > 1 and Cin_pad % 64 == 0, else [Cout][kh][kw][Cin_pad];
     zero padded to Kp % 32 == 0."""
     co, ci, kh, kw = w.shape
     cp = cin_pad or pad_channels(ci)
     t = torch.zeros((co, kh, kw, cp), dtype=F32)
     t[..., :ci] = w.permute(0, 2, 3, 1).float()
-    if kh * kw > 1 and cp % 32 == 0:
-        t = t.reshape(co, kh, kw, cp // 32, 32).permute(0, 3, 1, 2, 4).contiguous()
+    if kh * kw > 1 and cp % 64 == 0:
+        t = t.reshape(co, kh, kw, cp // 64, 64).permute(0, 3, 1, 2, 4).contiguous()
     k = kh * kw * cp
     kp = (k + 31) // 32 * 32
     out = torch.zeros((co, kp), dtype=F16)

@@ -50,17 +50,20 @@ def test_pack_conv_layout():
 
 
 def test_pack_conv_channel_block_major():
-    """Cin % 32 == 0, 3x3: K order [Cin/32][kh][kw][32] (rdmi.h conv weight layout)."""
+    """Cin % 64 == 0, 3x3: K order [Cin/64][kh][kw][64] (rdmi.h conv weight layout)."""
     from rollingdepth_amd import kernels as K
 
-    w = torch.randn(4, 64, 3, 3)
+    w = torch.randn(4, 128, 3, 3)
     p = K.pack_conv(w, "cpu")
-    assert p.shape == (4, 576)
-    t = p.float().view(4, 2, 3, 3, 32)
+    assert p.shape == (4, 1152)
+    t = p.float().view(4, 2, 3, 3, 64)
     for cb in range(2):
         for dy in range(3):
             for dx in range(3):
-                assert torch.equal(t[:, cb, dy, dx], w[:, cb * 32:(cb + 1) * 32, dy, dx].half().float())
+                assert torch.equal(t[:, cb, dy, dx], w[:, cb * 64:(cb + 1) * 64, dy, dx].half().float())
+    # Cin % 64 != 0 keeps the tap-major order
+    w3 = torch.randn(2, 32, 3, 3)
+    assert torch.equal(K.pack_conv(w3, "cpu").float().view(2, 3, 3, 32), w3.permute(0, 2, 3, 1).half().float())
     # 1x1 kernels keep the plain [Cout][Cin] order
     w1 = torch.randn(3, 64, 1, 1)
     assert torch.equal(K.pack_conv(w1, "cpu").float(), w1[:, :, 0, 0].half().float())

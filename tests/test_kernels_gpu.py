@@ -21,7 +21,7 @@ def _k():
 @pytest.fixture(params=["auto", "classic", "pingpong"])
 def engine(request, monkeypatch):
     """GEMM/conv engine: by size (auto), the 3-slot classic engine only, or the ping-pong engine
-    forced for every N % 128 == 0 launch (RDMI_GEMM_PP, gemm.hip)."""
+    forced for every launch it supports (N % 256 == 0; RDMI_GEMM_PP, gemm.hip)."""
     monkeypatch.setenv("RDMI_GEMM_PP", {"auto": "1", "classic": "0", "pingpong": "2"}[request.param])
     return request.param
 
@@ -83,7 +83,8 @@ def test_gemm_geglu(engine):
     (1, 9, 7, 64, 64, 3, 1, 1, True), (2, 10, 10, 3, 32, 3, 1, 1, False), (1, 8, 8, 64, 4, 3, 1, 1, False),
     (2, 11, 13, 40, 24, 1, 1, 0, False), (2, 20, 18, 256, 256, 3, 1, 1, False), (1, 17, 15, 128, 128, 3, 1, 1, True),
     (2, 14, 14, 8, 128, 3, 1, 1, False), (1, 13, 11, 320, 640, 3, 2, 1, False), (2, 9, 10, 512, 512, 3, 1, 1, True),
-    (1, 12, 12, 40, 256, 3, 1, 1, False)])
+    (1, 12, 12, 40, 256, 3, 1, 1, False), (1, 13, 11, 64, 256, 3, 2, 1, False), (2, 7, 9, 192, 256, 3, 1, 1, True),
+    (1, 15, 17, 64, 512, 1, 1, 0, False)])
 def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(3)
