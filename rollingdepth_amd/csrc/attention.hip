@@ -2,14 +2,14 @@
 //
 // attn_fwd_d64: flash-style fused softmax(q kᵀ·scale) v for head_dim 64 on gfx950.
 //   Workgroup = 8 waves × 32 queries (256 queries) of one (batch, head); 128-key K/V tiles arrive
-//   by LDS-DMA into a 3-slot ring (two tiles in flight; K XOR-swizzled per 16-B chunk through the
-//   source address).
+//   by LDS-DMA into a 5-slot ring (K XOR-swizzled per 16-B chunk through the source address); the
+//   two halves of the workgroup run staggered by one barrier (MFMA block ∥ softmax block).
 //   Per wave and tile: Sᵀ = K·Qᵀ with v_mfma_f32_32x32x16_f16 (Q fragments live in registers for
 //   the whole sweep), so each lane owns one query's scores ("swapped QKᵀ": the row max/sum is
 //   lane-local plus one lane^32 exchange); Oᵀ = Vᵀ·Pᵀ with the P accumulator re-used directly
 //   as the B operand (keys in the MFMA's permuted k order) and V read from LDS with
-//   ds_read_b64_tr_b16 (hardware transpose).  Online softmax in exp2 domain, f32 throughout; the
-//   O rescale is skipped (exactly) on tiles where no lane's running max moved.
+//   ds_read_b64_tr_b16 (hardware transpose).  Online softmax in exp2 domain with the running max
+//   folded into the QKᵀ MFMA chain (details at the kernel).
 // attn_smallkv: attention of every query token against ≤ 16 shared keys (the UNet's
 //   cross-attention to the 2-token empty-text context) — a streaming kernel, no MFMA.
 // softmax_rows: f32 scores → f16 probabilities, for the d=C single-head VAE attention that is
@@ -32,22 +32,43 @@ constexpr int NKB = KB / 32;  // 32-key MFMA blocks per tile
 constexpr int DPW = KB / 8 / NWV;  // 8-row DMA instructions per wave per tile, per tensor
 constexpr int TILE = KB * 64; // halves per K (or V) tile
 
-__device__ f16x8 g_attn_zero16;
-
 template <int N>
 __device__ __forceinline__ void attn_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-// K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4) into a 3-slot ring (no VGPR staging,
+// K/V tiles arrive by LDS-DMA (buffer_load_dwordx4 … lds) into a 5-slot ring (no VGPR staging,
 // no ds_write): each wave moves 8 key rows of K and of V per tile.  K's 16-B chunks are
-// XOR-swizzled by (key & 7) through the per-lane source address; V stays row-major for the
-// transposed reads.
+// XOR-swizzled by (key & 7) through the per-lane source offset; V stays row-major for the
+// transposed reads.  Keys past Sk fall outside the buffer descriptors' range and read as zeros.
+//
+// Softmax VALU budget.  Q is prescaled by scale·log2(e) once, and the running row maximum m is
+// folded into the Sᵀ = K·Qᵀ MFMA chain as a 65th head dimension: K' = [K | 1], Q' = [Q | -m̃]
+// (one extra 32x32x16 MFMA per key block whose A operand is the constant "ones" column and whose
+// B operand carries -m̃ in f16), so the MFMA delivers S' = scores − m̃ directly and each score costs
+// only exp2, one add (row sum) and half a cvt_pk.  m̃ is kept as an f16 value (softmax is
+// shift-invariant, so any m̃ works as long as O and l share it).  It is set exactly on the first
+// tile and re-set — with the O/l rescale — only when a tile's row sum over this lane's 64 keys
+// exceeds 2^15 (the f16 range of P), i.e. when the row max grew by more than ≈9 (log2 units);
+// otherwise P stays bounded by 2^15 and f16 P keeps its relative precision.
+//
+// MFMA/VALU overlap.  Per tile t a wave runs an MFMA block M(t) = {Oᵀ += Vᵀ·P(t-1)ᵀ; S'(t) =
+// K'(t)·Q'ᵀ} (36 MFMAs) and a VALU block S(t) = {softmax of S'(t) → P(t); DMA}, separated by
+// barriers.  Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave is in its MFMA
+// block while its partner is in its VALU block (guide §5.5 T16 / MI355X_MICROARCH "Two waves per
+// SIMD").  With interval i between barriers, group g runs M(t) in interval 2t+g and S(t) in
+// 2t+1+g; K(t) is read in M(t), V(t) in M(t+1), so slot t is busy until interval 2t+3.
+// DMA(t) is issued in S(t-3) and each wave waits for it in S(t-2) (before the barrier that
+// precedes M(t) in both groups); it overwrites tile t-5, whose last read (M(t-4), group 1) ended
+// in interval 2t-7 < 2t-5.
+constexpr int NSLOT = 5;
+
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
-  __shared__ __attribute__((aligned(16))) f16 lds[3 * 2 * TILE];  // 96 KB: slot s = [K | V]
+  __shared__ __attribute__((aligned(16))) f16 lds[NSLOT * 2 * TILE];  // 160 KB: slot s = [K | V]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  const int grp = wid >> 2;
   const int hh = lane >> 5;  // lane half
   const int c = lane & 31;
   const int head = blockIdx.y;
@@ -55,36 +76,48 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   const int qi = blockIdx.x * QB + wid * 32 + c;
 
   const f16* Q = p.q + (long)b * p.q_bs + head * 64;
-  const f16* K = p.k + (long)b * p.k_bs + head * 64;
-  const f16* V = p.v + (long)b * p.v_bs + head * 64;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.k + (long)b * p.k_bs + head * 64), (short)0, (int)(((long)(p.Sk - 1) * p.k_ld + 64) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.v + (long)b * p.v_bs + head * 64), (short)0, (int)(((long)(p.Sk - 1) * p.v_ld + 64) * 2), 0x00020000);
 
-  // Q as the B operand of Sᵀ = K·Qᵀ: lane holds Q[qi][16ks + 8hh + 0..7]
+  // Q as the B operand of Sᵀ = K·Qᵀ: lane holds Q[qi][16ks + 8hh + 0..7] · scale·log2(e)
   f16x8 qf[4];
+  const f16 qs = (f16)p.sl2;
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     f16x8 z = {};
     qf[ks] = qi < p.Sq ? *(const f16x8*)(Q + (long)qi * p.q_ld + ks * 16 + hh * 8) : z;
+    qf[ks] *= qs;
   }
+  // the 65th dimension: A = ones column (k index 0 of the lanes < 32), B = -m̃ (same slot)
+  f16x8 ones = {}, qaug = {};
+  if (hh == 0) ones[0] = (f16)1.f;
 
-  // DMA lane geometry: 8 rows x 8 chunks per 1-KiB instruction; row = wid*8 + drow.
+  // DMA lane geometry: 8 rows x 8 chunks per 1-KiB instruction; row = (i*NWV + wid)*8 + drow.
   // LDS images (bank-conflict-free for the fragment reads, checked with SQ_LDS_BANK_CONFLICT):
   //   K: phys chunk = logical ^ ((row >> 1) & 7)   (ds_read_b128 of 16 distinct rows / group)
   //   V: phys chunk = logical ^ (((row >> 1) & 1) << 2)   (tr reads of 4 rows x 64 B / half-wave)
   const int drow = lane >> 3;
-  const f16* zero = (const f16*)&g_attn_zero16;
-  auto issue = [&](int kt, int slot) {
+  unsigned koff[DPW], voff[DPW];
+#pragma unroll
+  for (int i = 0; i < DPW; ++i) {
+    const int row = (i * NWV + wid) * 8 + drow;
+    const int kchunk = (lane & 7) ^ ((row >> 1) & 7);
+    const int vchunk = (lane & 7) ^ (((row >> 1) & 1) << 2);
+    koff[i] = (unsigned)(row * p.k_ld + kchunk * 8) * 2u;
+    voff[i] = (unsigned)(row * p.v_ld + vchunk * 8) * 2u;
+  }
+  const unsigned kstep = (unsigned)(KB * p.k_ld * 2), vstep = (unsigned)(KB * p.v_ld * 2);
+  auto issue = [&](int kt) {
+    const int slot = kt % NSLOT;
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
-      const int row = (i * NWV + wid) * 8 + drow;  // (row >> 1) & 7 depends on drow and wid only
-      const int kchunk = (lane & 7) ^ ((row >> 1) & 7);
-      const int vchunk = (lane & 7) ^ (((row >> 1) & 1) << 2);
-      const int key = kt * KB + row;
-      const bool ok = key < p.Sk;
       f16* ks_ = lds + slot * 2 * TILE + (i * NWV + wid) * 8 * 64;
-      __builtin_amdgcn_global_load_lds(ok ? (const void*)(K + (long)key * p.k_ld + kchunk * 8) : (const void*)zero,
-                                       (__attribute__((address_space(3))) void*)ks_, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(ok ? (const void*)(V + (long)key * p.v_ld + vchunk * 8) : (const void*)zero,
-                                       (__attribute__((address_space(3))) void*)(ks_ + TILE), 16, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)ks_, 16,
+                                               koff[i] + (unsigned)kt * kstep, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(ks_ + TILE), 16,
+                                               voff[i] + (unsigned)kt * vstep, 0, 0, 0);
     }
   };
 
@@ -93,96 +126,153 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   for (int d = 0; d < 2; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  float mt = 0.f, l = 0.f;  // m̃ (an f16 value, held in f32) and this lane's half of the row sum
 
   const int nt = (p.Sk + KB - 1) / KB;
   // tr-read lane geometry (16-lane groups)
   const int gi = lane >> 4, li = lane & 15;
   const int tr_key = 4 * (gi >> 1) + (li >> 2);
   const int tr_col = 16 * (gi & 1) + 4 * (li & 3);
-  issue(0, 0);
-  issue(1, 1);  // zero rows when nt == 1: keeps exactly 2·DPW younger DMAs in flight at every wait
+  const f32x16 zero16 = {};
+  f16x8 pf[2 * NKB] = {};
+
+  // Oᵀ += Vᵀ · Pᵀ for the tile in slot `slot` (KB/16 k-steps of 16 keys, 2 d-blocks of 32).
+  // The transposed V reads are inline asm: with the ds_read_tr builtin hipcc assumes the read may
+  // alias the in-flight LDS-DMA and drains vmcnt(0) before it, which serialises the K/V prefetch.
+  // Reads run two k-steps ahead of the MFMAs, each consumer behind a counted lgkmcnt.
+  auto pv = [&](int slot) {
+    const unsigned vbase = (unsigned)(uintptr_t)LDS_PTR(f16, lds + slot * 2 * TILE + TILE);
+    unsigned vaddr[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      // row = 16st + tr_key (+8): (row >> 1) & 1 == (tr_key >> 1) & 1 for both reads
+      const int col = d * 32 + tr_col;
+      const int pc = ((col >> 3) ^ (((tr_key >> 1) & 1) << 2)) << 3 | (col & 7);
+      vaddr[d] = vbase + (unsigned)((tr_key * 64 + pc) * 2);
+    }
+    i16x4 vr[3][4];  // [stage][d*2 + lo/hi]
+    auto rd = [&](int st, int buf) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(vr[buf][2 * d]) : "v"(vaddr[d]), "i"(st * 16 * 64 * 2));
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+                     : "=v"(vr[buf][2 * d + 1]) : "v"(vaddr[d]), "i"((st * 16 + 8) * 64 * 2));
+      }
+    };
+    rd(0, 0);
+    rd(1, 1);
+#pragma unroll
+    for (int st = 0; st < 2 * NKB; ++st) {
+      if (st + 1 < 2 * NKB)
+        asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // stage st landed (st+1 in flight)
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int buf = st % 3;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const f16x8 vf = __builtin_bit_cast(
+            f16x8, __builtin_shufflevector(vr[buf][2 * d], vr[buf][2 * d + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+        o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[st], o[d], 0, 0, 0);
+      }
+      if (st + 2 < 2 * NKB) rd(st + 2, (st + 2) % 3);
+    }
+  };
+
+  // prologue: DMA(0..2) issued ("S(-3..-1)"), DMA(0) and DMA(1) waited ("S(-2), S(-1)")
+  issue(0);
+  issue(1);
+  issue(2);
+  attn_wait_vmcnt<2 * DPW>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+  asm volatile("" ::: "memory");
 
   for (int kt = 0; kt < nt; ++kt) {
-    attn_wait_vmcnt<2 * DPW>();  // this wave's DMAs of tile kt landed (tile kt+1 in flight)
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's DMAs of kt landed; every wave done with kt-1
-    asm volatile("" ::: "memory");
-    issue(kt + 2, (kt + 2) % 3);   // past the end: zero rows into the drained slot
-    const f16* ks_ = lds + (kt % 3) * 2 * TILE;
-    const f16* vs_ = ks_ + TILE;
-    // ---- Sᵀ = K · Qᵀ for NKB key blocks of 32
+    // ================= M(kt): PV of the previous tile, S' of this tile.  The s_setprio pair keeps
+    // hipcc from moving the block's MFMAs across the barriers (guide §5.5 T5).
+    __builtin_amdgcn_s_setprio(1);
+    if (kt > 0) pv((kt - 1) % NSLOT);
+    const f16* ks_ = lds + (kt % NSLOT) * 2 * TILE;
     f32x16 s[NKB];
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
       const int key = kb * 32 + c;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int ch = 2 * ks + hh;
         f16x8 kf = *(const f16x8*)(ks_ + key * 64 + ((ch ^ ((key >> 1) & 7)) << 3));
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], s[kb], 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], ks ? s[kb] : zero16, 0, 0, 0);
       }
+      // last in the chain (a distinct accumulator input per block: no CSE into register copies)
+      s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones, qaug, s[kb], 0, 0, 0);
     }
-    // ---- mask + online softmax (lane owns query c, keys (r&3)+8(r>>2)+4hh of each block)
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // ================= S(kt): softmax → P(kt); DMA(kt+3); wait DMA(kt+2)
+    issue(kt + 3);  // past the end: zero rows into a drained slot
+    // ---- mask (last tile only; lane owns query c, keys (r&3)+8(r>>2)+4hh of each block)
     const int kbase = kt * KB;
-    float mx = -INFINITY;
-    if (kbase + KB <= p.Sk) {
-#pragma unroll
-      for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-    } else {
+    if (kbase + KB > p.Sk) {
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int key = kbase + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
           if (key >= p.Sk) s[kb][r] = -INFINITY;
-          mx = fmaxf(mx, s[kb][r]);
         }
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mn = fmaxf(m, mx);
-    // exact T13: rescale O only when some lane's running max moved (alpha == 1 otherwise)
-    if (__any(mn > m)) {
-      const float alpha = __builtin_amdgcn_exp2f((m - mn) * p.sl2);
+    // ---- P = exp2(S'), row sum
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(s[kb][r]);  // v_exp_f32, no denorm fixup
+        rs += e;
+        pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
+      }
+    // ---- (re)set m̃: always on the first tile, else only when P would leave the f16 range
+    if (kt == 0 || __any(!(rs <= 32768.f))) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (kt != 0) mx = fmaxf(mx, 0.f);               // never lower m̃ (l >= 1 stays true)
+      const float mnew = (float)(f16)(mt + mx);       // next m̃, an f16 value
+      const float delta = mnew - mt;                  // exact: both are f16 values
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
       l *= alpha;
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-      m = mn;
+      mt = mnew;
+      qaug[0] = hh == 0 ? (f16)(-mnew) : (f16)0.f;
+      rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(s[kb][r] - delta);
+          rs += e;
+          pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
+        }
     }
-    const float msc = m * p.sl2;
-    float rs = 0.f;
-    f16x8 pf[2 * NKB];
-#pragma unroll
-    for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float e = __builtin_amdgcn_exp2f(fmaf(s[kb][r], p.sl2, -msc));  // v_exp_f32, no denorm fixup
-        rs += e;
-        pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
-      }
     l += rs;
-    // ---- Oᵀ += Vᵀ · Pᵀ (KB/16 k-steps of 16 keys, 2 d-blocks of 32)
-#pragma unroll
-    for (int st = 0; st < 2 * NKB; ++st) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        // row = 16st + tr_key (+8): (row >> 1) & 1 == (tr_key >> 1) & 1 for both reads
-        const int col = d * 32 + tr_col;
-        const int pc = ((col >> 3) ^ (((tr_key >> 1) & 1) << 2)) << 3 | (col & 7);
-        const f16* base = vs_ + (16 * st + tr_key) * 64 + pc;
-        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, base));
-        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(i16x4, base + 8 * 64));
-        const f16x8 vf = __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        o[d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[st], o[d], 0, 0, 0);
-      }
-    }
+    attn_wait_vmcnt<2 * DPW>();  // DMA(kt+2) landed (DMA(kt+3) in flight)
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
+  // ================= M(nt): PV of the last tile
+  pv((nt - 1) % NSLOT);
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   attn_wait_vmcnt<0>();  // drain trailing zero-row DMAs before the workgroup retires
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = 1.f / lt;

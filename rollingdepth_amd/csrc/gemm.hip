@@ -143,10 +143,10 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
         }
       }
     }
-  } else {
+  } else if constexpr (WTN == 64) {
     // GEGLU: within each wave's WTN(=64)-column slab, columns [0,32) are the value half and
     // [32,64) the gate half of output columns slab*32 + [0,32) (N % 128 == 0: always vector).
-    static_assert(WTN == 64, "GEGLU slabs are 64 columns");
+    // (Launches with other wave widths never carry the GEGLU epilogue: launch_mode.)
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
       const int m = mw + i * 16 + fr;
@@ -383,26 +383,30 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
 
 // ---------------------------------------------------------------------------------------------
 // Ping-pong engine for the large launches (the VAE / UNet convolutions, big Linear layers).
-// 256×256 tile, 8 waves (2 M × 4 N), each wave a 128×64 output sub-tile (8×4 16×16 f32
-// accumulators).  K advances in 64-wide K-tiles (one full 128-B line per operand row) through a
-// 2-slot LDS ring (2 × 64 KiB) filled by LDS-DMA.  Each K-tile is four phases of 16 MFMAs per
-// wave:  p0 = (A rows 0-63 of the wave, k 0-31), p1 = (rows 0-63, k 32-63), p2 = (rows 64-127,
-// k 0-31), p3 = (rows 64-127, k 32-63); the B fragments of both k halves are read in p0/p1 and
-// stay in registers for p2/p3.  The two wave groups (waves 0-3 and 4-7: one wave per SIMD each)
-// run one barrier apart, so on every SIMD one wave issues its 16 MFMAs while the other issues its
-// ds_reads, address arithmetic and LDS-DMA for a later K-tile (guide §5 "256² 8-phase template":
-// ping-pong, s_setprio around the MFMAs, counted vmcnt, raw s_barrier).
-// Every load section first issues its fragment reads, then 2 DMA instructions per wave (8 per
-// K-tile: B halves B0/B1, A halves A0 = rows 0-63, A1 = rows 64-127 of each wave row), 3-5 phases
-// ahead of their first read:
-//   LOAD(4u)   : A0(u+1)          LOAD(4u+1): wait A1(u) (vmcnt 6), A1(u+1)
-//   LOAD(4u+2) : B0(u+2)          LOAD(4u+3): wait B(u+1), A0(u+1) (vmcnt 4), B1(u+2)
-// with LOAD(q) the load section of phase q = 4·(K-tile) + p.  RAW: each wave's wait sits in the
-// load section before the first read of the data, which is followed by a barrier that every
-// reader (either group) passes first.  WAR: B(u) and A0(u) are last read in LOAD(4u+1), which ends
-// with s_waitcnt lgkmcnt(0) before its barrier, so B(u)'s region is free from the next phase on in
-// either group (the groups are one barrier apart): B0(u+2) lands there in LOAD(4u+2), B1(u+2) in
-// LOAD(4u+3), A0(u+2) in LOAD(4u+4); A1(u+2) overwrites A1(u), last read in LOAD(4u+3), in
+// Tile BM×BN = (WM·128)×(WN·RN·16) with 8 waves as WM × WN (WM·WN = 8), each wave a 128×(16·RN)
+// output sub-tile (8×RN 16×16 f32 accumulators): 256×256 (WM 2, RN 4) and 512×128 (WM 4, RN 4:
+// the VAE's 128-channel convs).  (RN 5 — 256×320 for the UNet's 320-multiples — needs more than
+// the 256 registers of a 2-wave/SIMD kernel: hipcc moves the accumulators to scratch.)  K advances in
+// 64-wide K-tiles (one full 128-B line per operand row) through a 2-slot LDS ring filled by
+// LDS-DMA.  Each K-tile is four phases of 4·RN MFMAs per wave:  p0 = (A rows 0-63 of the wave,
+// k 0-31), p1 = (rows 0-63, k 32-63), p2 = (rows 64-127, k 0-31), p3 = (rows 64-127, k 32-63);
+// the B fragments of both k halves are read in p0/p1 and stay in registers for p2/p3.  The two
+// wave groups (waves 0-3 and 4-7: one wave per SIMD each) run one barrier apart, so on every SIMD
+// one wave issues its MFMAs while the other issues its ds_reads, address arithmetic and LDS-DMA
+// for a later K-tile (guide §5 "256² 8-phase template": ping-pong, s_setprio around the MFMAs,
+// counted vmcnt, raw s_barrier).
+// Every load section first issues its fragment reads, then its share of the DMA (per wave and
+// K-tile: NA pieces of A rows 0-63 of every wave row (A0), NA of rows 64-127 (A1), NB of B; one
+// piece = one 1-KiB instruction), ahead of their first read by 3-6 phases:
+//   LOAD(4u)  : A0b(u+1)                 LOAD(4u+1): wait A1(u), A1(u+1)
+//   LOAD(4u+2): B0(u+2)                  LOAD(4u+3): wait B(u+1)+A0(u+1), B1(u+2), A0a(u+2)
+// with LOAD(q) the load section of phase q = 4·(K-tile) + p, A0 = A0a (first A0A pieces) + A0b,
+// B = B0 (first NB0 pieces) + B1.  RAW: each wave's wait sits in the load section before the
+// first read of the data, which is followed by a barrier that every reader (either group) passes
+// first.  WAR: B(u) and A0(u) are last read in LOAD(4u+1), which ends with s_waitcnt lgkmcnt(0)
+// before its barrier, so their regions are free from the next phase on in either group (the
+// groups are one barrier apart): B0(u+2) lands there in LOAD(4u+2), B1(u+2)/A0a(u+2) in
+// LOAD(4u+3), A0b(u+2) in LOAD(4u+4); A1(u+2) overwrites A1(u), last read in LOAD(4u+3), in
 // LOAD(4u+5).  Past the last K-tile the DMAs read zero chunks (out-of-range offsets) so the vmcnt
 // arithmetic stays uniform.
 // LDS row images are 128 B (64 halves); 16-B chunk c of row r is stored at c ^ (r & 7) (source
@@ -411,19 +415,25 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
 // Conv (MODE 1/2) needs the channel-block-major K order with 64-channel blocks (p.cmaj): K-tile u
 // is tap u % 9 of channels 64·(u / 9) .. +63.
 // DBG (ablation builds only, RDMI_GEMM_DBG): bit0 no main-loop DMA, bit1 no barriers in the loop,
-// bit2 no ds_reads in the loop, bit3 no MFMAs.  Results are garbage; timings isolate the skeleton's costs.
-template <int MODE, int DBG = 0>
+// bit2 no ds_reads in the loop, bit3 no MFMAs.  Results are garbage; timings isolate the costs.
+template <int MODE, int WM, int RN, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
-  constexpr int BM = 256, BN = 256, BKP = 64;
-  constexpr int RM = 8, RN = 4;
-  constexpr int SLOT = (BM + BN) * BKP;  // halves (64 KiB)
+  constexpr int WN = 8 / WM;
+  constexpr int BM = WM * 128, BN = WN * RN * 16, BKP = 64;
+  constexpr int RM = 8;
+  constexpr int NA = WM;                 // A pieces per half per wave
+  constexpr int NB = BN / 64;            // B pieces per wave
+  constexpr int A0A = NA > 2 ? NA / 2 : 0;  // A0 pieces issued one phase early (LOAD(4u+3))
+  constexpr int NB0 = NB > 2 ? 2 : 1;
+  constexpr int SLOT = (BM + BN) * BKP;  // halves
+  static_assert(WM * WN == 8 && 2 * SLOT * 2 <= 163840, "tile does not fit");
   __shared__ __attribute__((aligned(16))) f16 lds[2 * SLOT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int grp = wid >> 2;
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WN, wn = wid % WN;
   const int nbx = gridDim.x;
   const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
   int mt_, nt_;
@@ -438,13 +448,13 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 
   // DMA lane geometry: one 1-KiB instruction = 8 rows × 128 B; lane → (row lrow, phys chunk lane&7)
   const int lrow = lane >> 3;
-  const int chunk = (lane & 7) ^ lrow;  // logical chunk fetched (row & 7 == lrow: piece rows start at multiples of 8)
-  // A pieces of this wave: half h, e = 0/1 → tile rows (t>>3)*128 + h*64 + (t&7)*8, t = wid + 8e
-  int arow[2][2], ahb[2][2], awb[2][2];
+  const int chunk = (lane & 7) ^ lrow;  // logical chunk fetched (piece rows start at multiples of 8)
+  // A pieces of this wave: half h, t = wid + 8e → tile rows (t>>3)*128 + h*64 + (t&7)*8 + lrow
+  int arow[2][NA], ahb[2][NA], awb[2][NA];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < NA; ++e) {
       const int t = wid + 8 * e;
       const int m = m0 + (t >> 3) * 128 + h * 64 + (t & 7) * 8 + lrow;
       const bool ok = m < p.M;
@@ -465,21 +475,23 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
         arow[h][e] = mm * (int)p.lda;
       }
     }
-  int brow[4];
+  int brow[NB];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < NB; ++e) {
     const int n = n0 + (wid + 8 * e) * 8 + lrow;
     brow[e] = n < p.N ? n * (int)p.ldw : -1;
   }
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
 
-  auto issueA = [&](int h, int u) {
+  // A pieces e in [e0, e1) of half h, K-tile u
+  auto issueA = [&](int h, int u, int e0, int e1) {
     f16* la = lds + (u & 1) * SLOT;
     if (MODE == 0) {
       const int kk = u * BKP + chunk * 8;
       const bool kok = kk < p.Kvalid;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int e = 0; e < NA; ++e) {
+        if (e < e0 || e >= e1) continue;
         const int t = wid + 8 * e;
         const bool ok = ahb[h][e] == 0 && kok;
         dma16(ra_, ok ? (unsigned)(arow[h][e] + kk) * 2u : OOB,
@@ -493,7 +505,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       const int cofs = cb * 64 + chunk * 8;
       const int tapoff = (dy * p.IW + dx) * p.Cin + cofs;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int e = 0; e < NA; ++e) {
+        if (e < e0 || e >= e1) continue;
         const int t = wid + 8 * e;
         const int hi = ahb[h][e] + dy, wi = awb[h][e] + dx;
         const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
@@ -506,12 +519,14 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       }
     }
   };
-  auto issueB = [&](int hb, int u) {  // B pieces e = 2hb, 2hb+1 of K-tile u
+  // B pieces e in [e0, e1) of K-tile u
+  auto issueB = [&](int u, int e0, int e1) {
     const int kk = u * BKP + chunk * 8;
     const bool kok = kk < p.Kvalid;
     f16* lb = lds + (u & 1) * SLOT + BM * BKP;
 #pragma unroll
-    for (int e = 2 * hb; e < 2 * hb + 2; ++e) {
+    for (int e = 0; e < NB; ++e) {
+      if (e < e0 || e >= e1) continue;
       const bool ok = brow[e] >= 0 && kok;
       dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 8 * e) * 8 * BKP);
     }
@@ -529,23 +544,22 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
   const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
 
-  // prologue: K-tile 0 whole, B of K-tile 1; wait for B(0) + A0(0)
-  issueB(0, 0);
-  issueB(1, 0);
-  issueA(0, 0);
-  issueA(1, 0);
-  issueB(0, 1);
-  issueB(1, 1);
-  wait_vmcnt<6>();
+  // prologue: the steady-state issue sequence up to iteration 0; then B(0) and A0(0) landed
+  issueB(0, 0, NB);
+  issueA(0, 0, 0, NA);
+  issueA(1, 0, 0, NA);
+  issueB(1, 0, NB);
+  issueA(0, 1, 0, A0A);
+  wait_vmcnt<NA + NB + A0A>();
   asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // K-tile 0 (B, A first half) visible to every wave
+  __builtin_amdgcn_s_barrier();  // K-tile 0 (B, A0) visible to every wave
   if (grp == 1 && !(DBG & 2)) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   asm volatile("" ::: "memory");
 
   f16x8 af[4] = {}, bf[2][RN] = {};
   for (int u = 0; u < nk; ++u) {
     const f16* la = lds + (u & 1) * SLOT + (wm * 128) * BKP;
-    const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * 64) * BKP;
+    const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * RN * 16) * BKP;
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
       const int h = ph >> 1, kh = ph & 1;
@@ -567,15 +581,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
       }
       if (!(DBG & 1)) {
         if (ph == 0) {
-          issueA(0, u + 1);
+          issueA(0, u + 1, A0A, NA);  // A0b(u+1)
         } else if (ph == 1) {
-          wait_vmcnt<6>();  // A1(u) landed (B(u+1), A0(u+1) in flight)
-          issueA(1, u + 1);
+          wait_vmcnt<NA + NB>();  // A1(u) landed (B(u+1), A0(u+1) in flight)
+          issueA(1, u + 1, 0, NA);
         } else if (ph == 2) {
-          issueB(0, u + 2);
+          issueB(u + 2, 0, NB0);
         } else {
-          wait_vmcnt<4>();  // B(u+1), A0(u+1) landed (A1(u+1), B0(u+2) in flight)
-          issueB(1, u + 2);
+          wait_vmcnt<NA + NB0>();  // B(u+1), A0(u+1) landed (A1(u+1), B0(u+2) in flight)
+          issueB(u + 2, NB0, NB);
+          issueA(0, u + 2, 0, A0A);
         }
       }
       // the last reads of B and A0 (p1) retire before the barrier: B0(u+2) re-fills B(u)'s region
@@ -607,35 +622,65 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   if (grp == 0 && !(DBG & 2)) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  store_tile<RM, RN, 64>(p, acc, m0 + wm * 128, n0 + wn * 64, bz, fr, fq);
+  store_tile<RM, RN, RN * 16>(p, acc, m0 + wm * 128, n0 + wn * RN * 16, bz, fr, fq);
 }
 
-
 // Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
-// engine only, 2 = ping-pong engine for every N % 128 == 0 launch, unset/1 = by size.
+// engine only, 2 = a ping-pong tile whenever the shape allows one, unset/1 = by estimated cost.
 int pp_mode() {
   const char* e = getenv("RDMI_GEMM_PP");
   return e ? atoi(e) : 1;
 }
 
+// Relative cost of a launch on an engine: rounds of one tile per CU × tile area ÷ measured
+// efficiency (tools/kbench.py on MI355X: ping-pong ≈ 1.3× the classic 256×128 engine per tile area).
+double tile_cost(long tiles, int bm, int bn, double eff) {
+  return (double)((tiles + 255) / 256) * bm * bn / eff;
+}
+
+template <int MODE, int WM, int RN>
+void launch_pp(const GemmP& p, int batch, hipStream_t s) {
+  constexpr int BM = WM * 128, BN = (8 / WM) * RN * 16;
+  dim3 g(p.N / BN, rdmi::div_up(p.M, BM), batch);
+  hipLaunchKernelGGL((gemm_pp_kernel<MODE, WM, RN>), g, dim3(512), 0, s, p);
+}
+
 template <int MODE>
 void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
   const int pp = pp_mode();
-  const long mt256 = (p.M + 255) / 256;
-  // measured (tools/kbench.py, MI355X): the 256x256 ping-pong tile wins from about four waves of
-  // tiles on (RDMI_GEMM_PP=2: whenever the shape allows it)
-  const long min_tiles = pp == 2 ? 0 : 1024;
-  if (pp != 0 && p.N % 256 == 0 && (MODE == 0 || p.cmaj) && mt256 * (p.N / 256) * batch >= min_tiles) {
-    dim3 g(p.N / 256, rdmi::div_up(p.M, 256), batch);
+  // ping-pong candidates (N must be a multiple of the tile width; conv needs 64-channel blocks)
+  if (pp != 0 && (MODE == 0 || p.cmaj)) {
     const char* dbg = MODE == 0 ? getenv("RDMI_GEMM_DBG") : nullptr;
-    switch (dbg ? atoi(dbg) : 0) {
-      case 1: hipLaunchKernelGGL((gemm_pp_kernel<0, 1>), g, dim3(512), 0, s, p); return;
-      case 5: hipLaunchKernelGGL((gemm_pp_kernel<0, 5>), g, dim3(512), 0, s, p); return;
-      case 8: hipLaunchKernelGGL((gemm_pp_kernel<0, 8>), g, dim3(512), 0, s, p); return;
-      case 12: hipLaunchKernelGGL((gemm_pp_kernel<0, 12>), g, dim3(512), 0, s, p); return;
-      default: hipLaunchKernelGGL((gemm_pp_kernel<MODE>), g, dim3(512), 0, s, p); return;
+    if (dbg && p.N % 256 == 0) {
+      dim3 g(p.N / 256, rdmi::div_up(p.M, 256), batch);
+      switch (atoi(dbg)) {
+        case 1: hipLaunchKernelGGL((gemm_pp_kernel<0, 2, 4, 1>), g, dim3(512), 0, s, p); return;
+        case 5: hipLaunchKernelGGL((gemm_pp_kernel<0, 2, 4, 5>), g, dim3(512), 0, s, p); return;
+        case 8: hipLaunchKernelGGL((gemm_pp_kernel<0, 2, 4, 8>), g, dim3(512), 0, s, p); return;
+        case 12: hipLaunchKernelGGL((gemm_pp_kernel<0, 2, 4, 12>), g, dim3(512), 0, s, p); return;
+        default: break;
+      }
+    }
+    const long mt256 = rdmi::div_up(p.M, 256), mt512 = rdmi::div_up(p.M, 512);
+    const long ct = rdmi::div_up(p.N, 128);
+    const double classic = tile_cost(mt256 * ct * batch, 256, 128, 1.0);
+    double best = pp == 2 ? 1e300 : classic;
+    int pick = 0;
+    if (p.N % 256 == 0) {
+      const double c = tile_cost(mt256 * (p.N / 256) * batch, 256, 256, 1.3);
+      if (c < best) best = c, pick = 1;
+    }
+    if (p.N % 128 == 0) {
+      const double c = tile_cost(mt512 * (p.N / 128) * batch, 512, 128, 1.3);
+      if (c < best) best = c, pick = 3;
+    }
+    switch (pick) {
+      case 1: launch_pp<MODE, 2, 4>(p, batch, s); return;
+      case 3: launch_pp<MODE, 4, 4>(p, batch, s); return;
+      default: break;
     }
   }
+  const long mt256 = (p.M + 255) / 256;
   if (force128 || p.N % 128 == 0 || p.N > 512) {
     if (mt256 * ((p.N + 127) / 128) * batch >= 512) {  // enough tiles to fill the chip with 256-row tiles
       dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 256), batch);

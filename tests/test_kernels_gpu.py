@@ -228,6 +228,38 @@ def test_attention_softmax_rescale_branch():
     assert (o.float() - ref).abs().max().item() < 5e-3
 
 
+@pytest.mark.parametrize("qscale,S", [(6.0, 700), (0.02, 300), (-4.0, 1000)])
+def test_attention_large_and_tiny_scores(qscale, S):
+    """Score ranges far outside the first tile's max (|scores| up to ~±60 in log2 units: the m̃
+    re-set path fires on many tiles) and nearly uniform softmax (scores ≈ 0)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(12)
+    B, H = 1, 3
+    C = H * 64
+    q = (torch.randn(B, S, C, device=DEV, generator=g) * qscale).half()
+    k = torch.randn(B, S, C, device=DEV, generator=g).half()
+    v = torch.randn(B, S, C, device=DEV, generator=g).half()
+    o = K_.attention(q, k, v, H)
+    ref = _sdpa_ref(q, k, v, H)
+    assert (o.float() - ref).abs().max().item() < 5e-3
+
+
+def test_attention_growing_max():
+    """Key norms grow along the sequence so the row max rises by a few units per tile: the m̃
+    re-set (and O/l rescale) fires repeatedly at moderate jumps, never at the first tile only."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    B, S, H = 1, 1536, 2
+    C = H * 64
+    q = torch.randn(B, S, C, device=DEV, generator=g).half()
+    ramp = torch.linspace(0.2, 3.0, S, device=DEV)[None, :, None]
+    k = (torch.randn(B, S, C, device=DEV, generator=g) * ramp).half()
+    v = torch.randn(B, S, C, device=DEV, generator=g).half()
+    o = K_.attention(q, k, v, H)
+    ref = _sdpa_ref(q, k, v, H)
+    assert (o.float() - ref).abs().max().item() < 5e-3
+
+
 def test_attention_smallkv():
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(9)
