@@ -16,6 +16,7 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 

@@ -633,7 +633,8 @@ int pp_mode() {
 }
 
 // Relative cost of a launch on an engine: rounds of one tile per CU × tile area ÷ measured
-// efficiency (tools/kbench.py on MI355X: ping-pong ≈ 1.3× the classic 256×128 engine per tile area).
+// efficiency (tools/kbench.py on MI355X: the 256×256 ping-pong tile ≈ 1.3× the classic 256×128
+// engine per tile area, the 512×128 one ≈ 1.0×).
 double tile_cost(long tiles, int bm, int bn, double eff) {
   return (double)((tiles + 255) / 256) * bm * bn / eff;
 }
@@ -671,7 +672,7 @@ void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
       if (c < best) best = c, pick = 1;
     }
     if (p.N % 128 == 0) {
-      const double c = tile_cost(mt512 * (p.N / 128) * batch, 512, 128, 1.3);
+      const double c = tile_cost(mt512 * (p.N / 128) * batch, 512, 128, 1.0);  // measured ≈ classic per area
       if (c < best) best = c, pick = 3;
     }
     switch (pick) {

@@ -1,4 +1,8 @@
-"""Run the L0 cross-frame attention shape a few times (for rocprofv3 --pmc passes)."""
+"""Run one attention (or conv) shape a few times — a target for rocprofv3 PMC passes.
+
+    python tools/attn_probe.py [--what attn|conv] [--iters 5]"""
+import argparse
+import math
 import os
 import sys
 
@@ -7,16 +11,25 @@ import torch  # noqa: E402
 
 from rollingdepth_amd import kernels as K  # noqa: E402
 
-B, S, H = 2, 27648, 5
-C = H * 64
-qkv = torch.randn(B, S, 3 * C, device="cuda").half()
-out = torch.empty(B, S, C, device="cuda", dtype=torch.float16)
-for _ in range(3):
-    K.attention(qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:], H, out=out)
+ap = argparse.ArgumentParser()
+ap.add_argument("--what", default="attn")
+ap.add_argument("--iters", type=int, default=5)
+a = ap.parse_args()
+torch.manual_seed(0)
+if a.what == "attn":
+    B, S, H = 8, 27648, 5
+    C = H * 64
+    qkv = torch.randn(B, S, 3 * C, device="cuda").half()
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    out = torch.empty(B, S, C, device="cuda", dtype=torch.float16)
+    fn = lambda: K.attention(q, k, v, H, out=out)  # noqa: E731
+else:
+    B, H, W, ci, co = 8, 192, 192, 512, 512
+    x = torch.randn(B, H, W, ci, device="cuda").half()
+    w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
+    out = torch.empty(B, H, W, co, device="cuda", dtype=torch.float16)
+    fn = lambda: K.conv2d(x, w, co, 3, out=out)  # noqa: E731
+for _ in range(a.iters):
+    fn()
 torch.cuda.synchronize()
-x = torch.randn(8, 192, 192, 512, device="cuda").half()
-w = K.pack_conv(torch.randn(512, 512, 3, 3) / 48, "cuda", 512)
-for _ in range(3):
-    K.conv2d(x, w, 512, 3)
-torch.cuda.synchronize()
-print("ok")
+print("done")
