@@ -106,6 +106,17 @@ int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G,
                          const float* mean_rstd, const float* gamma, const float* beta, int silu,
                          void* stream);
 
+/* GroupNorm apply (+ SiLU when silu = 1) fused with a 3×3, stride-1, pad-1 convolution to ONE output
+ * channel: y[b, h, w] = bias + Σ_{dy,dx,c} w[3dy+dx][c] · n(x)[b, h+dy-1, w+dx-1, c], n = the
+ * normalised (+SiLU) input, zero outside the image.  x [B][H][W][C] f16, w [9][C] f32, y [B][H][W]
+ * f16, workspace ≥ rdmi_conv3x3_to1_gn_workspace(B, H, W) floats.  Replaces the decoder's
+ * conv_norm_out → conv_act → conv_out (vae.py:335-347) followed by the depth pipeline's mean over
+ * the RGB outputs (rollingdepth_pipeline.py:737), which is linear and folded into w / bias. */
+long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W);
+int rdmi_conv3x3_to1_gn(const void* x, int B, int H, int W, int C, int G, const float* mean_rstd,
+                        const float* gamma, const float* beta, int silu, const float* w, float bias,
+                        void* y, float* workspace, void* stream);
+
 /* LayerNorm over the last dim (BasicTransformerBlock.norm1/2/3, attention.py:445,495,522). */
 int rdmi_layernorm(const void* x, void* y, long M, int C, const float* gamma, const float* beta,
                    float eps, void* stream);

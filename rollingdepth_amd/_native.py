@@ -67,6 +67,8 @@ _SIGS = {
     "rdmi_groupnorm_stats": (i32, [vp, i32, i64, i32, i32, f32, vp, vp, vp]),
     "rdmi_groupnorm_stats_partials": (i32, [vp, i64, i32, i64, i32, i32, f32, vp, vp]),
     "rdmi_groupnorm_apply": (i32, [vp, vp, i32, i64, i32, i32, vp, vp, vp, i32, vp]),
+    "rdmi_conv3x3_to1_gn_workspace": (i64, [i32, i32, i32]),
+    "rdmi_conv3x3_to1_gn": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, f32, vp, vp, vp]),
     "rdmi_layernorm": (i32, [vp, vp, i64, i32, vp, vp, f32, vp]),
     "rdmi_attention_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i64, i64, i64,
                                  f32, vp]),

@@ -1,0 +1,107 @@
+// Decoder head: GroupNorm apply (+ SiLU) fused with the 3×3 convolution to ONE output channel
+// (vae.decoder.conv_norm_out → conv_act → conv_out, vae.py:335-347, with the depth pipeline's mean
+// over the three RGB outputs folded into the weights, rollingdepth_pipeline.py:737).
+//
+// A 1-channel 3×3 conv is HBM-bound, not MFMA-bound (2·9·C FLOPs per 2·C input bytes), and as an
+// implicit GEMM it wastes the 16-wide MFMA N dimension and re-reads every input line 9×.  Here
+// every input pixel is read once:
+//   pass 1 (one thread per input pixel p): y = silu(a·x[p] + s) in f32 (a, s per image and channel
+//           from the GroupNorm statistics), d[tap][p] = Σ_c y[c]·w[tap][c] for the 9 taps;
+//   pass 2 (one thread per output pixel q): out[q] = bias + Σ_tap d[tap][q + offset(tap)], taps
+//           outside the image contributing 0 (the conv's zero padding of the normalised input).
+// HBM bytes per pixel: 2·C read + 9·4 written + 9·4 read (L2-served neighbours) + 2 written,
+// against 4·C (GroupNorm apply) + 2·C + 2 for the separate apply → conv launches.
+#include "common.h"
+
+namespace {
+
+constexpr int HT = 256;  // threads per workgroup
+
+// pass 1: x [B][HW][C] f16, mr [B*G][2] {mean, rstd}, gamma/beta [C] f32, w [9][C] f32 → d [9][B*HW]
+__global__ __launch_bounds__(HT) void head_taps(const f16* __restrict__ x, long HW, int C, int G,
+                                                const float* __restrict__ mr, const float* __restrict__ gamma,
+                                                const float* __restrict__ beta, const float* __restrict__ w,
+                                                int silu, float* __restrict__ d, long P) {
+  extern __shared__ float sm[];  // sc[C], sh[C], w[9][C]
+  float* sc = sm;
+  float* sh = sc + C;
+  float* wl = sh + C;
+  const int b = blockIdx.y;
+  const int cpg = C / G;
+  for (int c = threadIdx.x; c < C; c += HT) {
+    const int g = c / cpg;
+    const float mean = mr[2 * (b * G + g)], rstd = mr[2 * (b * G + g) + 1];
+    sc[c] = rstd * gamma[c];
+    sh[c] = beta[c] - mean * sc[c];
+  }
+  for (int i = threadIdx.x; i < 9 * C; i += HT) wl[i] = w[i];
+  __syncthreads();
+  const long p = (long)blockIdx.x * HT + threadIdx.x;
+  if (p >= HW) return;
+  const f16* xp = x + ((long)b * HW + p) * C;
+  float acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+  for (int c0 = 0; c0 < C; c0 += 8) {
+    const f16x8 v = *(const f16x8*)(xp + c0);
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float f = fmaf((float)v[e], sc[c0 + e], sh[c0 + e]);
+      y[e] = silu ? silu_f(f) : f;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t] = fmaf(y[e], wl[t * C + c0 + e], acc[t]);
+  }
+  const long q = (long)b * HW + p;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) d[t * P + q] = acc[t];
+}
+
+// pass 2: out[b][h][w] = bias + Σ_{dy,dx} d[3dy+dx][b][h+dy-1][w+dx-1] (zero outside the image)
+__global__ __launch_bounds__(HT) void head_gather(const float* __restrict__ d, int H, int W, long P, float bias,
+                                                  f16* __restrict__ out) {
+  const long q = (long)blockIdx.x * HT + threadIdx.x;
+  if (q >= P) return;
+  const long HW = (long)H * W;
+  const long b = q / HW;
+  const int r = (int)(q - b * HW);
+  const int h = r / W, wc = r - (r / W) * W;
+  float s = bias;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int hh = h + dy - 1;
+    if ((unsigned)hh >= (unsigned)H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int ww = wc + dx - 1;
+      if ((unsigned)ww >= (unsigned)W) continue;
+      s += d[(3 * dy + dx) * P + b * HW + (long)hh * W + ww];
+    }
+  }
+  out[q] = (f16)s;
+}
+
+}  // namespace
+
+extern "C" long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W) { return 9L * B * H * W; }
+
+extern "C" int rdmi_conv3x3_to1_gn(const void* x, int B, int H, int W, int C, int G, const float* mean_rstd,
+                                   const float* gamma, const float* beta, int silu, const float* w, float bias,
+                                   void* y, float* workspace, void* stream) {
+  RDMI_REQUIRE(x && mean_rstd && gamma && beta && w && y && workspace, RDMI_E_ARG, "conv3x3_to1_gn: null pointer");
+  RDMI_REQUIRE(B > 0 && H > 0 && W > 0 && C % 8 == 0 && C > 0 && C <= 1024 && G > 0 && C % G == 0, RDMI_E_ARG,
+               "conv3x3_to1_gn: bad sizes B=%d H=%d W=%d C=%d G=%d", B, H, W, C, G);
+  RDMI_REQUIRE(((uintptr_t)x & 15) == 0, RDMI_E_ALIGN, "conv3x3_to1_gn: x not 16-byte aligned");
+  const long HW = (long)H * W, P = (long)B * HW;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = (size_t)11 * C * sizeof(float);
+  hipLaunchKernelGGL(head_taps, dim3(rdmi::div_up(HW, HT), B), dim3(HT), lds, s, (const f16*)x, HW, C, G, mean_rstd,
+                     gamma, beta, w, silu, workspace, P);
+  int rc = rdmi::check_launch("conv3x3_to1_gn taps");
+  if (rc) return rc;
+  hipLaunchKernelGGL(head_gather, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (f16*)y);
+  return rdmi::check_launch("conv3x3_to1_gn gather");
+}

@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -43,11 +44,16 @@ def profile_stop():
     return out
 
 
+_PROF_SHAPES = os.environ.get("RDMI_PROF_SHAPES") == "1"  # key the timings by launch shape too
+
+
 class _Timed:
     __slots__ = ("name", "flop", "ev")
 
-    def __init__(self, name, flop):
+    def __init__(self, name, flop, shape=None):
         self.name, self.flop, self.ev = name, flop, None
+        if _PROF_SHAPES and shape is not None:
+            self.name = f"{name} {shape}"
 
     def __enter__(self):
         if _PROF is not None:
@@ -143,7 +149,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     part = _gn_part(out, M, N) if (gn and batch == 1 and not geglu and not out_f32) else None
     if part is not None:
         g.gn_part, g.gn_ld = part.data_ptr(), part.stride(0)
-    with _Timed("implicit_gemm", 2.0 * M * N * k * batch):
+    with _Timed("implicit_gemm", 2.0 * M * N * k * batch, f"gemm M={M} N={N} K={k} b={batch}"):
         check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
     _gn_attach(out, part)
     return out
@@ -245,7 +251,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
         a.gn_part, a.gn_ld = _gn_slot
-    with _Timed("implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin):
+    with _Timed("implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin,
+                f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}"):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
     if _gn_slot is None:
         _gn_attach(out, part)
@@ -293,6 +300,27 @@ def groupnorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
     return out
 
 
+def conv3x3_to1_gn(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float, silu: bool,
+                   w9: torch.Tensor, bias: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GroupNorm(+SiLU) → 3×3 conv (pad 1) to one channel, fused (rdmi.h rdmi_conv3x3_to1_gn).
+    x NHWC f16 [B, H, W, C]; w9 f32 [9, C] (tap = 3·dy + dx); returns [B, H, W, 1] f16."""
+    _need(x, F16, "conv3x3_to1_gn.x")
+    _need(w9, F32, "conv3x3_to1_gn.w9")
+    B, H, W, C_ = x.shape
+    if w9.shape != (9, C_):
+        raise ValueError(f"conv3x3_to1_gn: w9 {tuple(w9.shape)} != (9, {C_})")
+    mr = groupnorm_stats(x, groups, eps)
+    out = torch.empty((B, H, W, 1), dtype=F16, device=x.device) if out is None else out
+    if out.numel() != B * H * W or not out.is_contiguous():
+        raise ValueError("conv3x3_to1_gn: out must be a contiguous [B, H, W, 1] tensor")
+    ws = _workspace(lib.rdmi_conv3x3_to1_gn_workspace(B, H, W), x.device)
+    with _Timed("conv_head", 2.0 * 9 * C_ * B * H * W, f"head B={B} {H}x{W} {C_}->1"):
+        check(lib.rdmi_conv3x3_to1_gn(x.data_ptr(), B, H, W, C_, groups, mr.data_ptr(), gamma.data_ptr(),
+                                      beta.data_ptr(), int(silu), w9.data_ptr(), float(bias), out.data_ptr(),
+                                      ws.data_ptr(), _stream()), "rdmi_conv3x3_to1_gn")
+    return out
+
+
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _need(x, F16, "layernorm.x")
@@ -318,7 +346,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
     if out is None:
         out = torch.empty((B, Sq, HD), dtype=F16, device=q.device)
     sc = 1.0 / math.sqrt(D) if scale is None else scale
-    with _Timed("attention_fwd", 4.0 * B * heads * Sq * Sk * D):
+    with _Timed("attention_fwd", 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}"):
         check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
                                      q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
                                      v.stride(0), out.stride(0), sc, _stream()), "rdmi_attention_fwd")

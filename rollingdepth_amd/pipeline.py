@@ -70,8 +70,8 @@ class RollingDepthPipeline:
         self.unet, self.vae, self.scheduler = unet, vae, scheduler
         self.text_encoder, self.tokenizer = text_encoder, tokenizer
         self.empty_text_embed: Optional[torch.Tensor] = None
-        self.snippet_batch = 8
-        self.vae_batch = 8
+        self.snippet_batch = 16  # snippets per UNet call (48 frames at snippet length 3)
+        self.vae_batch = 16      # frames per VAE encode / decode call
         self._dev = unet.dev
 
     # ------------------------------------------------------------------ construction

@@ -108,8 +108,12 @@ class VAE:
             self.d_up.append((res, us))
         self.d_norm = _Norm(sd, "decoder.conv_norm_out", dev)
         wd, bd = sd["decoder.conv_out.weight"], sd["decoder.conv_out.bias"]
-        self.d_out = _FoldedConv(wd.double().mean(0, keepdim=True).float(), bd.double().mean(0, keepdim=True).float(),
-                                 dev)
+        wm = wd.double().mean(0, keepdim=True).float()  # [1, C, 3, 3]
+        bm = bd.double().mean(0, keepdim=True).float()
+        self.d_out = _FoldedConv(wm, bm, dev)
+        # the same folded conv as the fused GroupNorm+SiLU+conv head's [tap][C] f32 weights
+        self.d_w9 = wm[0].permute(1, 2, 0).reshape(9, -1).contiguous().to(dev, F32)
+        self.d_b = float(bm[0])
         self.groups = g
 
     # ------------------------------------------------------------------ encode
@@ -151,5 +155,9 @@ class VAE:
                 h = r(h)
             if us is not None:
                 h = us(h, upsample=True, gn=True)
-        h = K.groupnorm(h, self.d_norm.g, self.d_norm.b, self.groups, 1e-6, silu=True)
-        return self.d_out(h, out=out)
+        # conv_norm_out → SiLU → conv_out (RGB mean folded) as one HBM pass over h (convhead.hip)
+        if out is not None and not out.is_contiguous():
+            h = K.groupnorm(h, self.d_norm.g, self.d_norm.b, self.groups, 1e-6, silu=True)
+            return self.d_out(h, out=out)
+        return K.conv3x3_to1_gn(h, self.d_norm.g, self.d_norm.b, self.groups, 1e-6, True, self.d_w9, self.d_b,
+                                out=out)

@@ -179,6 +179,26 @@ def test_groupnorm_moments_from_gemm(engine):
     assert (out.float() - ref).abs().max().item() < 1e-2
 
 
+@pytest.mark.parametrize("B,H,W,C,silu", [(2, 24, 20, 128, True), (1, 7, 9, 64, False), (3, 33, 17, 128, True)])
+def test_conv3x3_to1_gn(B, H, W, C, silu):
+    """Fused decoder head (convhead.hip) vs GroupNorm(+SiLU) → conv2d(pad 1) to one channel in fp32."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(14)
+    x = (torch.randn(B, H, W, C, device=DEV, generator=g) * 1.5 + 0.3).half()
+    gm = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
+    bt = 0.1 * torch.randn(C, device=DEV, generator=g)
+    w = torch.randn(1, C, 3, 3, device=DEV, generator=g) / math.sqrt(9 * C)
+    b = 0.3
+    w9 = w[0].permute(1, 2, 0).reshape(9, C).contiguous()
+    y = K_.conv3x3_to1_gn(x, gm, bt, 32, 1e-6, silu, w9, b)
+    n = F.group_norm(x.float().permute(0, 3, 1, 2), 32, gm, bt, 1e-6)
+    if silu:
+        n = F.silu(n)
+    ref = F.conv2d(n, w, torch.tensor([b], device=DEV), padding=1).permute(0, 2, 3, 1)
+    assert y.shape == (B, H, W, 1)
+    assert (y.float() - ref).abs().max().item() < 5e-3
+
+
 @pytest.mark.parametrize("C", [320, 640, 1280])
 def test_layernorm(C):
     K_ = _k()

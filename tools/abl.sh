@@ -1,4 +1,6 @@
 set -e
 mkdir -p gpurun_out
-for v in 0 1 2 3; do RDMI_ATTN_VAR=$v timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "attention" >> gpurun_out/abl_tests.log 2>&1; done
-for r in 1 2; do for v in 0 1 2 3; do echo "== VAR=$v" >> gpurun_out/abl.log; RDMI_ATTN_VAR=$v timeout -k 5 100 python tools/kbench.py --only attn >> gpurun_out/abl.log 2>&1; done; done
+for sb in 8 16; do for vb in 8 16; do
+  echo "== snippet_batch=$sb vae_batch=$vb" >> gpurun_out/abl.log
+  timeout -k 10 200 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --snippet-batch $sb --vae-batch $vb 2>&1 | grep metric | cut -c1-220 >> gpurun_out/abl.log
+done; done
