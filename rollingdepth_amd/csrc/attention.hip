@@ -165,12 +165,15 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     rd(1, 1);
 #pragma unroll
     for (int st = 0; st < 2 * NKB; ++st) {
+      const int buf = st % 3;
       if (st + 1 < 2 * NKB)
         asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");  // stage st landed (st+1 in flight)
       else
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the destinations count as written here, not at the issuing asm (guide §5.7 item 1 form ii):
+      // no compiler copy of them can be placed between the read and the wait
+      asm volatile("" : "+v"(vr[buf][0]), "+v"(vr[buf][1]), "+v"(vr[buf][2]), "+v"(vr[buf][3]));
       __builtin_amdgcn_sched_barrier(0);
-      const int buf = st % 3;
 #pragma unroll
       for (int d = 0; d < 2; ++d) {
         const f16x8 vf = __builtin_bit_cast(

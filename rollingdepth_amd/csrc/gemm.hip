@@ -47,9 +47,28 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f
 // Epilogue shared by both engines.  The MFMA ran as Dᵀ = W·Aᵀ, so a lane holds 4 CONSECUTIVE
 // output channels n = fq*4 + r of one row m = lane&15: bias / time-embedding / residual are read
 // and the result written as 4-element vectors (8-B f16 / 16-B f32), scalar only at a ragged N
-// tail.  mw/nw: the wave's first output row / column.
-template <int RM, int RN, int WTN>
-__device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], int mw, int nw, int bz, int fr, int fq) {
+// tail.  rows: the wave's output-row map (LinRows / PatchRows); nw: its first output column.
+// Output-row maps of a wave's 16-row fragments i (lane row fr): consecutive rows of the GEMM M
+// dimension, or the rows of a 16-pixel-wide spatial patch (conv_halo_kernel).  slot(i): the
+// 32-row GroupNorm-moment slot of the fragment pair (i-1, i) (rdmi.h gn_part); every image's slots
+// are the contiguous range [b·HW/32, (b+1)·HW/32) in both maps.
+struct LinRows {
+  int mw, fr, M;
+  __device__ int row(int i) const {
+    const int m = mw + i * 16 + fr;
+    return m < M ? m : -1;
+  }
+  __device__ long slot(int i) const { return (mw + (i - 1) * 16) >> 5; }
+};
+struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; Ho even, Wo % 16 == 0
+  int b, Ho, Wo, y0, x0, rw, fr;
+  __device__ int row(int i) const { return (b * Ho + y0 + rw + i) * Wo + x0 + fr; }
+  __device__ long slot(int i) const { return (long)((b * Ho + y0 + rw + i - 1) >> 1) * (Wo >> 4) + (x0 >> 4); }
+};
+
+template <int RM, int RN, int WTN, class Rows>
+__device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
+                                           int fr, int fq) {
   const long cb = (long)bz * p.sC;
   const long rbz = (long)bz * p.sR;
   if (!p.geglu) {
@@ -57,8 +76,8 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
     float gs[RN], gq[RN];  // per column tile: moments of this lane's 4 outputs over a 32-row block
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
-      const int m = mw + i * 16 + fr;
-      const bool mok = m < p.M;
+      const int m = rows.row(i);
+      const bool mok = m >= 0;
       const float* rbrow = p.rowbias && mok ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
       const long crow = cb + (long)m * p.ldc;
       const long rrow = rbz + (long)m * p.ldr;
@@ -135,7 +154,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
               q += __shfl_xor(q, o, 64);
             }
             if (fr == 0 && ok) {
-              float* d = p.gnp + (long)(n >> 2) * p.gn_ld + (long)((m - 16) >> 5) * 2;
+              float* d = p.gnp + (long)(n >> 2) * p.gn_ld + rows.slot(i) * 2;
               d[0] = s;
               d[1] = q;
             }
@@ -149,8 +168,8 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
     // (Launches with other wave widths never carry the GEGLU epilogue: launch_mode.)
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
-      const int m = mw + i * 16 + fr;
-      if (m >= p.M) continue;
+      const int m = rows.row(i);
+      if (m < 0) continue;
       const long crow = cb + (long)m * p.ldc;
 #pragma unroll
       for (int j = 0; j < RN / 2; ++j) {
@@ -378,7 +397,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(GemmP p) {
   }
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  store_tile<RM, RN, WTN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, bz, fr, fq);
+  store_tile<RM, RN, WTN>(p, acc, LinRows{m0 + wm * WTM, fr, p.M}, n0 + wn * WTN, bz, fr, fq);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -622,7 +641,204 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   if (grp == 0 && !(DBG & 2)) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  store_tile<RM, RN, RN * 16>(p, acc, m0 + wm * 128, n0 + wn * RN * 16, bz, fr, fq);
+  store_tile<RM, RN, RN * 16>(p, acc, LinRows{m0 + wm * 128, fr, p.M}, n0 + wn * RN * 16, bz, fr, fq);
+}
+
+// Halo ("direct") 3×3 convolution, stride 1, pad 1 (MODE 1), or through a nearest ×2 upsample
+// (MODE 2), for Cin % 64 == 0 and output sizes that tile into 16×16 patches.
+// The implicit GEMM above re-reads every input line for each of the 9 taps (9 A K-tiles per
+// 64-channel block, served by L2): its per-CU L2→LDS stream, not the MFMAs, sets its speed.  Here
+// a workgroup owns a 16×16 output-pixel patch × 256 output channels; per 64-channel block it loads
+// the 18×18-pixel input halo ONCE into LDS (40.5 KiB, one LDS-DMA pass) and reads the A fragments
+// of all 9 taps from it at shifted pixel positions; only the weights stream per tap (32 KiB).  Per
+// 64-channel block the workgroup moves 41 + 9·32 KiB instead of 9·(32 + 32) KiB (−43 %).
+// Structure: the 8-wave ping-pong of gemm_pp_kernel (2 M × 4 N waves, 128 pixels = 8 patch rows ×
+// 16 columns by 64 channels per wave, four phases of 16 MFMAs per K-tile, groups one barrier
+// apart); K-tile u = (channel block u / 9, tap u % 9) in the cmaj64 weight order.
+// LDS: two halo buffers (48 pieces of 8 pixels: 324 used) + a 2-slot weight ring = 160 KiB.
+// DMA per wave: per K-tile 4 weight pieces (B0 in LOAD(4u+2), B1 in LOAD(4u+3), for K-tile u+2);
+// per channel block cb, the 6 halo pieces of block cb+1 in LOAD(4u) of taps 1..6.
+// Waits (LOAD(4u+3)): B(u+1) landed — vmcnt(2), or vmcnt(3) when a halo piece was issued in
+// LOAD(4u); on tap 7 that wait also covers all of halo(cb+1), first read at tap 0 of block cb+1.
+// WAR: B(u+2) overwrites B(u), last read in LOAD(4u+1), which ends with lgkmcnt(0) (as in
+// gemm_pp_kernel); halo(cb+1) overwrites halo(cb-1), last read in the final K-tile of block cb-1,
+// ≥ 5 phases before tap 1 of block cb.
+// Halo LDS image: pixel hp = r·18 + c of the halo at 128 B, 16-B chunk k stored at k ^ (hp & 7)
+// (source-side swizzle): the 16 consecutive pixels of a fragment read are conflict-free for any
+// tap shift.  Halo pixels outside the image read as zeros (out-of-range buffer offsets) = padding.
+// NPH = phases per K-tile: 4 (16 MFMAs per phase, as gemm_pp_kernel) or 2 (32 MFMAs per phase:
+// both k halves of a row half; half the barriers, twice the work between them).  With NPH = 2 the
+// weights of K-tile u+2 are issued whole in LOAD(2u+1) after waiting for B(u+1) (vmcnt 0, or 1
+// with a halo piece in flight), B(u) having been last read in LOAD(2u), which ends with lgkmcnt(0).
+template <int MODE, int NPH>
+__global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
+  constexpr int BN = 256, BKP = 64, RM = 8, RN = 4;
+  constexpr int HWD = 18, HPIX = HWD * HWD;
+  constexpr int HPW = 6;                 // halo pieces per wave per channel block (48 >= 41)
+  constexpr int HALO = 48 * 8 * BKP;     // halves per halo buffer (48 KiB)
+  constexpr int BSLOT = BN * BKP;        // halves per weight slot (32 KiB)
+  __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + 2 * BSLOT];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int grp = wid >> 2;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int nbx = gridDim.x;
+  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+  int mt_, nt_;
+  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN;
+  const int pxn = p.Wo >> 4, pyn = p.Ho >> 4;
+  const int px = mt_ % pxn;
+  const int py = (mt_ / pxn) % pyn;
+  const int b = mt_ / (pxn * pyn);
+  const int y0 = py * 16, x0 = px * 16;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.Wt, (short)0, (int)p.w_bytes, 0x00020000);
+
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ lrow;  // logical chunk fetched: piece pixels start at multiples of 8
+  const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
+  // halo pieces of this wave: t = wid + 8e → halo pixels hp = 8t + lrow (hp < 324 used)
+  int hoff[HPW];
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    const int hp = (wid + 8 * e) * 8 + lrow;
+    const int hr = hp / HWD, hc = hp - hr * HWD;
+    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
+    const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
+    const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
+    hoff[e] = ok ? ((b * p.IH + sy) * p.IW + sx) * p.Cin : -1;
+  }
+  int brow[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int n = n0 + (wid + 8 * e) * 8 + lrow;
+    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+  }
+  const int ncb = p.Cin >> 6;
+  auto issueHalo = [&](int cb, int e) {
+    f16* lh = lds + (cb & 1) * HALO + (wid + 8 * e) * 8 * BKP;
+    const bool ok = hoff[e] >= 0 && cb < ncb;
+    dma16(ra_, ok ? (unsigned)(hoff[e] + cb * 64 + chunk * 8) * 2u : OOB, lh);
+  };
+  auto issueB = [&](int u, int e0, int e1) {
+    const int kk = u * BKP + chunk * 8;
+    const bool kok = kk < p.Kvalid;
+    f16* lb = lds + 2 * HALO + (u & 1) * BSLOT;
+#pragma unroll
+    for (int e = e0; e < e1; ++e) {
+      const bool ok = brow[e] >= 0 && kok;
+      dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 8 * e) * 8 * BKP);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = ncb * 9;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
+  const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+
+  // prologue: halo(0) and the weights of K-tiles 0 and 1; wait for halo(0) + B(0)
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) issueHalo(0, e);
+  issueB(0, 0, 4);
+  issueB(1, 0, 4);
+  wait_vmcnt<4>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
+  asm volatile("" ::: "memory");
+
+  constexpr int NKH = 4 / NPH;  // k halves per phase
+  const int wms = __builtin_amdgcn_readfirstlane(wm);
+  f16x8 af[NKH][4] = {}, bf[2][RN] = {};
+  for (int u = 0; u < nk; ++u) {
+    const int cb = u / 9;  // wave-uniform
+    const int tap = u - cb * 9;
+    const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+    const f16* lh = lds + (cb & 1) * HALO;
+    const f16* lb = lds + 2 * HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
+    const bool halo_now = tap >= 1 && tap <= HPW;
+    // halo pixel of fragment (h, i), lane fr: hp = (8wm + 4h + i + dy)·18 + dx + fr, whose swizzle
+    // term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or h
+    const int xb = fr + dx + 2 * dy;
+#pragma unroll
+    for (int ph = 0; ph < NPH; ++ph) {
+      const int h = NPH == 4 ? ph >> 1 : ph;
+      // ---- LOAD(NPH·u + ph): fragment reads, then waits / DMA
+#pragma unroll
+      for (int q = 0; q < NKH; ++q) {
+        const int kh = NPH == 4 ? (ph & 1) : q;
+        if (h == 0) {
+          const int off = kh ? off1 : off0;
+#pragma unroll
+          for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f16* row = lh + ((wms * 8 + h * 4 + i + dy) * HWD + dx) * BKP;
+          af[q][i] = *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
+        }
+      }
+      if (NPH == 4) {
+        if (ph == 0) {
+          if (halo_now) issueHalo(cb + 1, tap - 1);
+        } else if (ph == 2) {
+          issueB(u + 2, 0, 2);
+        } else if (ph == 3) {
+          if (halo_now)
+            wait_vmcnt<3>();  // B(u+1) landed (this tap's halo piece and B0(u+2) in flight)
+          else
+            wait_vmcnt<2>();  // B(u+1) (and on tap 7 all of halo(cb+1)) landed (B0(u+2) in flight)
+          issueB(u + 2, 2, 4);
+        }
+        if (ph == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        if (ph == 0) {
+          if (halo_now) issueHalo(cb + 1, tap - 1);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B(u) read for the last time
+        } else {
+          if (halo_now)
+            wait_vmcnt<1>();  // B(u+1) landed (this tap's halo piece in flight)
+          else
+            wait_vmcnt<0>();  // B(u+1) (and on tap 7 all of halo(cb+1)) landed
+          issueB(u + 2, 0, 4);
+        }
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // ---- MFMA(NPH·u + ph)
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int q = 0; q < NKH; ++q) {
+        const int kh = NPH == 4 ? (ph & 1) : q;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[h * 4 + i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[q][i], acc[h * 4 + i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
+  wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
+
+  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * 8, fr}, n0 + wn * 64, 0, fr, fq);
 }
 
 // Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
@@ -786,5 +1002,29 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
                RDMI_E_ARG, "conv2d: GroupNorm moments need vector output, Cout %% 4 == 0, B*Ho*Wo %% 32 == 0");
   p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 2);
   p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 2);
+  // halo engine: 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 patches,
+  // Cout % 256 == 0 (RDMI_CONV_HALO: 0 disables it, 1 = the 4-phase variant; for A/B measurements)
+  const char* he = getenv("RDMI_CONV_HALO");
+  const bool halo_ok = (!he || atoi(he) != 0) && p.cmaj && a->stride == 1 && a->pad_top == 1 && a->pad_left == 1 &&
+                       a->Ho % 16 == 0 && a->Wo % 16 == 0 && a->Cout % 256 == 0 && !p.rowbias &&
+                       a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
+  if (halo_ok) {
+    const char* gm = getenv("RDMI_GEMM_GROUP");
+    p.group_m = gm ? atoi(gm) : 8;
+    dim3 g(a->Cout / 256, (a->Ho / 16) * (a->Wo / 16) * a->B, 1);
+    const bool ph2 = !he || atoi(he) != 1;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
+    if (a->upsample) {
+      if (ph2)
+        hipLaunchKernelGGL((conv_halo_kernel<2, 2>), g, dim3(512), 0, (hipStream_t)stream, p);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<2, 4>), g, dim3(512), 0, (hipStream_t)stream, p);
+    } else {
+      if (ph2)
+        hipLaunchKernelGGL((conv_halo_kernel<1, 2>), g, dim3(512), 0, (hipStream_t)stream, p);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<1, 4>), g, dim3(512), 0, (hipStream_t)stream, p);
+    }
+    return rdmi::check_launch("conv2d halo");
+  }
   return launch(p, 1, (hipStream_t)stream, false, dense ? 0 : (a->upsample ? 2 : 1));
 }

@@ -18,11 +18,13 @@ def _k():
     return K
 
 
-@pytest.fixture(params=["auto", "classic", "pingpong"])
+@pytest.fixture(params=["auto", "classic", "pingpong", "halo4"])
 def engine(request, monkeypatch):
-    """GEMM/conv engine: by size (auto), the 3-slot classic engine only, or the ping-pong engine
-    forced for every launch it supports (N % 256 == 0; RDMI_GEMM_PP, gemm.hip)."""
-    monkeypatch.setenv("RDMI_GEMM_PP", {"auto": "1", "classic": "0", "pingpong": "2"}[request.param])
+    """GEMM/conv engine: by size (auto: halo conv with 2 phases per K-tile where it applies), the
+    3-slot classic engine only, the ping-pong engine forced for every launch it supports
+    (N % 256 == 0), or the 4-phase halo conv (RDMI_GEMM_PP / RDMI_CONV_HALO, gemm.hip)."""
+    monkeypatch.setenv("RDMI_GEMM_PP", {"auto": "1", "classic": "0", "pingpong": "2", "halo4": "1"}[request.param])
+    monkeypatch.setenv("RDMI_CONV_HALO", {"auto": "2", "classic": "0", "pingpong": "0", "halo4": "1"}[request.param])
     return request.param
 
 
@@ -84,7 +86,10 @@ def test_gemm_geglu(engine):
     (2, 11, 13, 40, 24, 1, 1, 0, False), (2, 20, 18, 256, 256, 3, 1, 1, False), (1, 17, 15, 128, 128, 3, 1, 1, True),
     (2, 14, 14, 8, 128, 3, 1, 1, False), (1, 13, 11, 320, 640, 3, 2, 1, False), (2, 9, 10, 512, 512, 3, 1, 1, True),
     (1, 12, 12, 40, 256, 3, 1, 1, False), (1, 13, 11, 64, 256, 3, 2, 1, False), (2, 7, 9, 192, 256, 3, 1, 1, True),
-    (1, 15, 17, 64, 512, 1, 1, 0, False)])
+    (1, 15, 17, 64, 512, 1, 1, 0, False),
+    # halo engine (3x3 s1 p1, Cin % 64 == 0, 16x16 output patches, Cout % 256 == 0)
+    (2, 32, 48, 128, 256, 3, 1, 1, False), (1, 16, 16, 64, 512, 3, 1, 1, False), (1, 8, 16, 192, 256, 3, 1, 1, True),
+    (3, 16, 32, 320, 256, 3, 1, 1, False)])
 def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(3)
@@ -135,7 +140,8 @@ def test_groupnorm(C, G, HW, silu, eps):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,up", [(2, 16, 16, 64, 128, False), (3, 12, 12, 128, 256, True),
-                                                (1, 24, 20, 256, 512, False)])
+                                                (1, 24, 20, 256, 512, False), (2, 16, 32, 128, 256, False),
+                                                (2, 8, 8, 64, 256, True)])
 def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine):
     """Conv epilogue-emitted GroupNorm moments (rdmi.h gn_part) vs the standalone stats pass and an
     fp32 reference; the moments of each image are bitwise independent of the batch they ran in."""
