@@ -670,20 +670,32 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 // both k halves of a row half; half the barriers, twice the work between them).  With NPH = 2 the
 // weights of K-tile u+2 are issued whole in LOAD(2u+1) after waiting for B(u+1) (vmcnt 0, or 1
 // with a halo piece in flight), B(u) having been last read in LOAD(2u), which ends with lgkmcnt(0).
-template <int MODE, int NPH>
+// WN = waves along N: 4 (256 output channels, waves of 8 patch rows × 64 channels) or 2 (128
+// output channels, waves of 4 patch rows × 64 channels; NPH = 1: one phase of 32 MFMAs per K-tile
+// and a 3-slot weight ring, since B(u) is read until the end of K-tile u: B(u+2) goes into the
+// slot of B(u-1) in LOAD(u), after the halo piece, and the wait for B(u+1) follows it (vmcnt 2,
+// or 3 with a halo piece); every load section ends with lgkmcnt(0)).
+template <int MODE, int NPH, int WN>
 __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
-  constexpr int BN = 256, BKP = 64, RM = 8, RN = 4;
+  constexpr int WM = 8 / WN;
+  constexpr int BN = WN * 64, BKP = 64, RM = 16 / WM, RN = 4;
+  constexpr int NRG = NPH == 4 ? 2 : NPH;  // row groups of a wave (one per phase group)
+  constexpr int RPG = RM / NRG;            // patch rows per row group
+  constexpr int NKH = NPH == 4 ? 1 : 2;    // k halves per phase
+  constexpr int NB = BN / 64;              // weight pieces per wave per K-tile
+  constexpr int NBS = NPH == 1 ? 3 : 2;    // weight ring slots
   constexpr int HWD = 18, HPIX = HWD * HWD;
-  constexpr int HPW = 6;                 // halo pieces per wave per channel block (48 >= 41)
-  constexpr int HALO = 48 * 8 * BKP;     // halves per halo buffer (48 KiB)
-  constexpr int BSLOT = BN * BKP;        // halves per weight slot (32 KiB)
-  __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + 2 * BSLOT];
+  constexpr int HPW = 6;                   // halo pieces per wave per channel block (48 >= 41)
+  constexpr int HALO = 48 * 8 * BKP;       // halves per halo buffer (48 KiB)
+  constexpr int BSLOT = BN * BKP;          // halves per weight slot
+  static_assert(RPG == 4 && (NPH != 1 || WN == 2) && (WN != 2 || NPH == 1), "unsupported halo variant");
+  __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + NBS * BSLOT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int grp = wid >> 2;
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WN, wn = wid % WN;
   const int nbx = gridDim.x;
   const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
   int mt_, nt_;
@@ -713,9 +725,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
     hoff[e] = ok ? ((b * p.IH + sy) * p.IW + sx) * p.Cin : -1;
   }
-  int brow[4];
+  int brow[NB];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < NB; ++e) {
     const int n = n0 + (wid + 8 * e) * 8 + lrow;
     brow[e] = n < p.N ? n * (int)p.ldw : -1;
   }
@@ -728,7 +740,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   auto issueB = [&](int u, int e0, int e1) {
     const int kk = u * BKP + chunk * 8;
     const bool kok = kk < p.Kvalid;
-    f16* lb = lds + 2 * HALO + (u & 1) * BSLOT;
+    f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT;
 #pragma unroll
     for (int e = e0; e < e1; ++e) {
       const bool ok = brow[e] >= 0 && kok;
@@ -750,15 +762,14 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   // prologue: halo(0) and the weights of K-tiles 0 and 1; wait for halo(0) + B(0)
 #pragma unroll
   for (int e = 0; e < HPW; ++e) issueHalo(0, e);
-  issueB(0, 0, 4);
-  issueB(1, 0, 4);
-  wait_vmcnt<4>();
+  issueB(0, 0, NB);
+  issueB(1, 0, NB);
+  wait_vmcnt<NB>();
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   asm volatile("" ::: "memory");
 
-  constexpr int NKH = 4 / NPH;  // k halves per phase
   const int wms = __builtin_amdgcn_readfirstlane(wm);
   f16x8 af[NKH][4] = {}, bf[2][RN] = {};
   for (int u = 0; u < nk; ++u) {
@@ -766,26 +777,26 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     const int tap = u - cb * 9;
     const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
     const f16* lh = lds + (cb & 1) * HALO;
-    const f16* lb = lds + 2 * HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
+    const f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT + (wn * 64) * BKP;
     const bool halo_now = tap >= 1 && tap <= HPW;
-    // halo pixel of fragment (h, i), lane fr: hp = (8wm + 4h + i + dy)·18 + dx + fr, whose swizzle
-    // term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or h
+    // halo pixel of fragment row r = RM·wm + 4·rg + i, lane fr: hp = (r + dy)·18 + dx + fr, whose
+    // swizzle term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or rg (RM·18, 72 ≡ 0 mod 8)
     const int xb = fr + dx + 2 * dy;
 #pragma unroll
     for (int ph = 0; ph < NPH; ++ph) {
-      const int h = NPH == 4 ? ph >> 1 : ph;
+      const int rg = NPH == 4 ? ph >> 1 : ph;
       // ---- LOAD(NPH·u + ph): fragment reads, then waits / DMA
 #pragma unroll
       for (int q = 0; q < NKH; ++q) {
         const int kh = NPH == 4 ? (ph & 1) : q;
-        if (h == 0) {
+        if (rg == 0) {
           const int off = kh ? off1 : off0;
 #pragma unroll
           for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const f16* row = lh + ((wms * 8 + h * 4 + i + dy) * HWD + dx) * BKP;
+          const f16* row = lh + ((wms * RM + rg * 4 + i + dy) * HWD + dx) * BKP;
           af[q][i] = *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
         }
       }
@@ -802,7 +813,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
           issueB(u + 2, 2, 4);
         }
         if (ph == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      } else {
+      } else if (NPH == 2) {
         if (ph == 0) {
           if (halo_now) issueHalo(cb + 1, tap - 1);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B(u) read for the last time
@@ -811,8 +822,16 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
             wait_vmcnt<1>();  // B(u+1) landed (this tap's halo piece in flight)
           else
             wait_vmcnt<0>();  // B(u+1) (and on tap 7 all of halo(cb+1)) landed
-          issueB(u + 2, 0, 4);
+          issueB(u + 2, 0, NB);
         }
+      } else {
+        if (halo_now) issueHalo(cb + 1, tap - 1);
+        issueB(u + 2, 0, NB);  // into the slot of B(u-1), read for the last time in LOAD(u-1)
+        if (halo_now)
+          wait_vmcnt<NB + 1>();  // B(u+1) landed (halo piece, B(u+2) in flight)
+        else
+          wait_vmcnt<NB>();  // B(u+1) (and on tap 7 all of halo(cb+1)) landed (B(u+2) in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -826,8 +845,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < RN; ++j)
-            acc[h * 4 + i][j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[q][i], acc[h * 4 + i][j], 0, 0, 0);
+            acc[rg * 4 + i][j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[q][i], acc[rg * 4 + i][j], 0, 0, 0);
       }
       __builtin_amdgcn_s_setprio(0);
       asm volatile("" ::: "memory");
@@ -838,7 +857,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   if (grp == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * 8, fr}, n0 + wn * 64, 0, fr, fq);
+  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq);
 }
 
 // Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
@@ -1003,26 +1022,37 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 2);
   p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 2);
   // halo engine: 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 patches,
-  // Cout % 256 == 0 (RDMI_CONV_HALO: 0 disables it, 1 = the 4-phase variant; for A/B measurements)
+  // Cout % 256 == 0 or 128 (RDMI_CONV_HALO: 0 disables it, 1 = the 4-phase variant; A/B measurements)
   const char* he = getenv("RDMI_CONV_HALO");
-  const bool halo_ok = (!he || atoi(he) != 0) && p.cmaj && a->stride == 1 && a->pad_top == 1 && a->pad_left == 1 &&
-                       a->Ho % 16 == 0 && a->Wo % 16 == 0 && a->Cout % 256 == 0 && !p.rowbias &&
+  const int hmode = he ? atoi(he) : 2;
+  const bool halo_ok = hmode != 0 && p.cmaj && a->stride == 1 && a->pad_top == 1 && a->pad_left == 1 &&
+                       a->Ho % 16 == 0 && a->Wo % 16 == 0 && (a->Cout % 256 == 0 || a->Cout == 128) && !p.rowbias &&
                        a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
   if (halo_ok) {
     const char* gm = getenv("RDMI_GEMM_GROUP");
     p.group_m = gm ? atoi(gm) : 8;
-    dim3 g(a->Cout / 256, (a->Ho / 16) * (a->Wo / 16) * a->B, 1);
-    const bool ph2 = !he || atoi(he) != 1;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
-    if (a->upsample) {
-      if (ph2)
-        hipLaunchKernelGGL((conv_halo_kernel<2, 2>), g, dim3(512), 0, (hipStream_t)stream, p);
-      else
-        hipLaunchKernelGGL((conv_halo_kernel<2, 4>), g, dim3(512), 0, (hipStream_t)stream, p);
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
+    if (a->Cout % 256 == 0) {
+      dim3 g(a->Cout / 256, patches, 1);
+      const bool ph2 = hmode != 1;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
+      if (a->upsample) {
+        if (ph2)
+          hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4>), g, dim3(512), 0, st, p);
+        else
+          hipLaunchKernelGGL((conv_halo_kernel<2, 4, 4>), g, dim3(512), 0, st, p);
+      } else {
+        if (ph2)
+          hipLaunchKernelGGL((conv_halo_kernel<1, 2, 4>), g, dim3(512), 0, st, p);
+        else
+          hipLaunchKernelGGL((conv_halo_kernel<1, 4, 4>), g, dim3(512), 0, st, p);
+      }
     } else {
-      if (ph2)
-        hipLaunchKernelGGL((conv_halo_kernel<1, 2>), g, dim3(512), 0, (hipStream_t)stream, p);
+      dim3 g(1, patches, 1);
+      if (a->upsample)
+        hipLaunchKernelGGL((conv_halo_kernel<2, 1, 2>), g, dim3(512), 0, st, p);
       else
-        hipLaunchKernelGGL((conv_halo_kernel<1, 4>), g, dim3(512), 0, (hipStream_t)stream, p);
+        hipLaunchKernelGGL((conv_halo_kernel<1, 1, 2>), g, dim3(512), 0, st, p);
     }
     return rdmi::check_launch("conv2d halo");
   }

@@ -89,7 +89,7 @@ def test_gemm_geglu(engine):
     (1, 15, 17, 64, 512, 1, 1, 0, False),
     # halo engine (3x3 s1 p1, Cin % 64 == 0, 16x16 output patches, Cout % 256 == 0)
     (2, 32, 48, 128, 256, 3, 1, 1, False), (1, 16, 16, 64, 512, 3, 1, 1, False), (1, 8, 16, 192, 256, 3, 1, 1, True),
-    (3, 16, 32, 320, 256, 3, 1, 1, False)])
+    (3, 16, 32, 320, 256, 3, 1, 1, False), (2, 32, 16, 128, 128, 3, 1, 1, False), (1, 16, 8, 256, 128, 3, 1, 1, True)])
 def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(3)
@@ -141,7 +141,7 @@ def test_groupnorm(C, G, HW, silu, eps):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,up", [(2, 16, 16, 64, 128, False), (3, 12, 12, 128, 256, True),
                                                 (1, 24, 20, 256, 512, False), (2, 16, 32, 128, 256, False),
-                                                (2, 8, 8, 64, 256, True)])
+                                                (2, 8, 8, 64, 256, True), (2, 16, 32, 128, 128, False)])
 def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine):
     """Conv epilogue-emitted GroupNorm moments (rdmi.h gn_part) vs the standalone stats pass and an
     fp32 reference; the moments of each image are bitwise independent of the batch they ran in."""
