@@ -84,8 +84,16 @@ typedef struct rdmi_conv_args {
   int B, H, W, Cin, Cout, kh, kw, stride, pad_top, pad_left, upsample, Ho, Wo, Kp;
   long y_ld; long res_ld; float alpha; long rowbias_ld; /* 0: one row shared by all images */
   float* gn_part; long gn_ld; /* GroupNorm moments of y, laid out as in rdmi_gemm_args; rows = B·Ho·Wo */
+  /* GroupNorm (+SiLU) of the INPUT applied as x is read (the norm1/norm2 → conv1/conv2 pairs of
+   * ResnetBlock2D, resnet.py:326-352): the conv sees silu?(x·sc + sh) with sc = rstd·gamma[c],
+   * sh = beta[c] − mean·sc per image b (in_mean_rstd as rdmi_groupnorm_stats writes it), the
+   * padding still zero; the same values rdmi_groupnorm_apply writes.  NULL in_mean_rstd: off.
+   * Shapes that support it: rdmi_conv2d_in_gn_supported (otherwise RDMI_E_UNSUPPORTED). */
+  const float* in_mean_rstd; const float* in_gamma; const float* in_beta; int in_groups, in_silu;
 } rdmi_conv_args;
 int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
+/* 1 if rdmi_conv2d fuses an input GroupNorm for this shape (in_groups set; pointers not read) */
+int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* args);
 
 /* ---------------------------------------------------------------------------------------
  * GroupNorm on NHWC f16: statistics then apply (optionally fused SiLU).

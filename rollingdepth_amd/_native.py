@@ -41,6 +41,7 @@ class ConvArgs(C.Structure):
         ("Kp", i32),
         ("y_ld", i64), ("res_ld", i64), ("alpha", f32), ("rowbias_ld", i64),
         ("gn_part", vp), ("gn_ld", i64),
+        ("in_mean_rstd", vp), ("in_gamma", vp), ("in_beta", vp), ("in_groups", i32), ("in_silu", i32),
     ]
 
 
@@ -63,6 +64,7 @@ _SIGS = {
     "rdmi_version": (i32, []),
     "rdmi_gemm": (i32, [C.POINTER(GemmArgs), vp]),
     "rdmi_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
+    "rdmi_conv2d_in_gn_supported": (i32, [C.POINTER(ConvArgs)]),
     "rdmi_groupnorm_workspace": (i64, [i32, i32]),
     "rdmi_groupnorm_stats": (i32, [vp, i32, i64, i32, i32, f32, vp, vp, vp]),
     "rdmi_groupnorm_stats_partials": (i32, [vp, i64, i32, i64, i32, i32, f32, vp, vp]),

@@ -39,7 +39,12 @@ inline int div_up(long a, long b) { return (int)((a + b - 1) / b); }
     }                                        \
   } while (0)
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// x·σ(x) with the hardware exp2 and reciprocal (≈2 ulp f32; the f16 outputs it feeds round far
+// coarser): 7 VALU ops instead of the ≈16 of an IEEE division.  exp2(+inf) = inf → rcp → 0 → −0
+// for very negative x, as silu.
+__device__ __forceinline__ float silu_f(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -30,6 +30,8 @@ struct GemmP {
   int cmaj;  // weights / K order channel-block major (rdmi.h): K-tile = one tap of 64 channels
   float* gnp; long gn_ld;  // GroupNorm moments of the output (32 rows x 4 channels), or null
   int group_m;  // tile order inside an XCD's range: groups of group_m m-tiles, n-tiles within a group
+  // GroupNorm (+SiLU) of the conv INPUT, applied as it is read (conv_halo_kernel<..., GN = true>)
+  const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
 };
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
@@ -655,7 +657,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 // Structure: the 8-wave ping-pong of gemm_pp_kernel (2 M × 4 N waves, 128 pixels = 8 patch rows ×
 // 16 columns by 64 channels per wave, four phases of 16 MFMAs per K-tile, groups one barrier
 // apart); K-tile u = (channel block u / 9, tap u % 9) in the cmaj64 weight order.
-// LDS: two halo buffers (48 pieces of 8 pixels: 324 used) + a 2-slot weight ring = 160 KiB.
+// LDS: two halo buffers (41 pieces of 8 pixels: 324 used; of the 48 piece slots of 8 waves × 6,
+// slots ≥ 41 are not loaded) + a 2-slot weight ring = 146 KiB (+ 8 KiB GroupNorm table).
 // DMA per wave: per K-tile 4 weight pieces (B0 in LOAD(4u+2), B1 in LOAD(4u+3), for K-tile u+2);
 // per channel block cb, the 6 halo pieces of block cb+1 in LOAD(4u) of taps 1..6.
 // Waits (LOAD(4u+3)): B(u+1) landed — vmcnt(2), or vmcnt(3) when a halo piece was issued in
@@ -675,7 +678,19 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 // and a 3-slot weight ring, since B(u) is read until the end of K-tile u: B(u+2) goes into the
 // slot of B(u-1) in LOAD(u), after the halo piece, and the wait for B(u+1) follows it (vmcnt 2,
 // or 3 with a halo piece); every load section ends with lgkmcnt(0)).
-template <int MODE, int NPH, int WN>
+// GN: the input is the raw tensor under a GroupNorm (+SiLU) (ResnetBlock2D norm1/norm2 → conv1/
+// conv2, resnet.py:326-352): each wave normalises the halo pieces it loaded, in place in LDS, with
+// the per-channel scale/shift of its image (table in LDS, built in the prologue from mean/rstd,
+// gamma, beta; the same f32 formula as rdmi_groupnorm_apply, so the result is identical to the
+// unfused pair).  Piece e of halo(cb+1), issued in tap e+1, has landed by the wait of tap e+2 and
+// is normalised inside the wave's own MFMA segments — channels 0-3 in phase 1 of tap e+2, 4-7 in
+// phase 0 of tap e+3 (NPH 1: all in tap e+2) — as VALU work between its MFMAs, which the matrix
+// pipe runs concurrently (normalising in the load segments instead, as extra work on the critical
+// path, cost as much as the separate apply pass it replaces: tools/kbench.py gnconv).  The segment
+// ends with lgkmcnt(0); the last write (tap 8 phase 0) is ≥ 2 barriers before the first read of
+// block cb+1 by the group running one barrier ahead.  Halo pixels outside the image stay zero (the conv's zero padding is
+// applied after the norm).  Halo(0) is normalised in the prologue.
+template <int MODE, int NPH, int WN, bool GN>
 __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   constexpr int WM = 8 / WN;
   constexpr int BN = WN * 64, BKP = 64, RM = 16 / WM, RN = 4;
@@ -685,11 +700,15 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   constexpr int NB = BN / 64;              // weight pieces per wave per K-tile
   constexpr int NBS = NPH == 1 ? 3 : 2;    // weight ring slots
   constexpr int HWD = 18, HPIX = HWD * HWD;
-  constexpr int HPW = 6;                   // halo pieces per wave per channel block (48 >= 41)
-  constexpr int HALO = 48 * 8 * BKP;       // halves per halo buffer (48 KiB)
+  constexpr int HPW = 6;                   // halo piece slots per wave per channel block (48 >= 41)
+  constexpr int HPC = 41;                  // pieces holding halo pixels (41·8 = 328 >= 324)
+  constexpr int HALO = HPC * 8 * BKP;      // halves per halo buffer (41 KiB)
   constexpr int BSLOT = BN * BKP;          // halves per weight slot
-  static_assert(RPG == 4 && (NPH != 1 || WN == 2) && (WN != 2 || NPH == 1), "unsupported halo variant");
-  __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + NBS * BSLOT];
+  constexpr int GNT = GN ? 1024 : 0;       // GroupNorm scale/shift table: sc[1024], sh[1024] floats
+  static_assert(RPG == 4 && (NPH != 1 || WN == 2) && (WN != 2 || NPH == 1) && (!GN || NPH != 4),
+                "unsupported halo variant");
+  __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + NBS * BSLOT + 4 * GNT];
+  float* const gnt = (float*)(lds + 2 * HALO + NBS * BSLOT);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -732,6 +751,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     brow[e] = n < p.N ? n * (int)p.ldw : -1;
   }
   const int ncb = p.Cin >> 6;
+  const int wids = __builtin_amdgcn_readfirstlane(wid);
+  auto hv = [&](int e) { return wids + 8 * e < HPC; };  // piece slot e of this wave holds halo pixels
   auto issueHalo = [&](int cb, int e) {
     f16* lh = lds + (cb & 1) * HALO + (wid + 8 * e) * 8 * BKP;
     const bool ok = hoff[e] >= 0 && cb < ncb;
@@ -759,12 +780,65 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
   const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
 
+  // in-place GroupNorm (+SiLU) of half hf (4 channels) of this wave's piece e of halo(cbn): lane
+  // data = 8 channels of logical chunk `chunk` of one halo pixel (the DMA wrote lane L's 16 B at
+  // piece + 16·L)
+  auto xform = [&](int cbn, int e, int hf) {
+    f16* lh = lds + (cbn & 1) * HALO + (wid + 8 * e) * 8 * BKP + lane * 8 + hf * 4;
+    const float* ts = gnt + cbn * 64 + chunk * 8 + hf * 4;
+    const f32x4 sc = *(const f32x4*)ts, sh = *(const f32x4*)(ts + GNT);
+    const f16x4 v = *(const f16x4*)lh;
+    const bool in = hoff[e] >= 0;
+    f16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float f = fmaf((float)v[i], sc[i], sh[i]);
+      if (p.gsilu) f = silu_f(f);
+      o[i] = in ? (f16)f : (f16)0.f;
+    }
+    *(f16x4*)lh = o;
+  };
+
   // prologue: halo(0) and the weights of K-tiles 0 and 1; wait for halo(0) + B(0)
 #pragma unroll
-  for (int e = 0; e < HPW; ++e) issueHalo(0, e);
+  for (int e = 0; e < HPW; ++e)
+    if (hv(e)) issueHalo(0, e);
   issueB(0, 0, NB);
+  float gmean[2] = {0.f, 0.f}, grstd[2] = {0.f, 0.f}, ggam[2] = {0.f, 0.f}, gbet[2] = {0.f, 0.f};
+  if constexpr (GN) {  // mean/rstd, gamma, beta of image b's channels (loads overlap the DMA latency)
+    const int cpg = p.Cin / p.gG;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = tid + 512 * r;
+      if (c < p.Cin) {
+        const int g = c / cpg;
+        gmean[r] = p.gmr[2 * (b * p.gG + g)];
+        grstd[r] = p.gmr[2 * (b * p.gG + g) + 1];
+        ggam[r] = p.ggam[c];
+        gbet[r] = p.gbet[c];
+      }
+    }
+  }
   issueB(1, 0, NB);
   wait_vmcnt<NB>();
+  if constexpr (GN) {  // scale/shift table (the formula of rdmi_groupnorm_apply)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float sc = grstd[r] * ggam[r];
+      gnt[tid + 512 * r] = sc;
+      gnt[GNT + tid + 512 * r] = gbet[r] - gmean[r] * sc;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int e = 0; e < HPW; ++e)
+      if (hv(e)) {
+        xform(0, e, 0);
+        xform(0, e, 1);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
@@ -778,14 +852,18 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
     const f16* lh = lds + (cb & 1) * HALO;
     const f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT + (wn * 64) * BKP;
-    const bool halo_now = tap >= 1 && tap <= HPW;
+    const bool halo_now = tap >= 1 && tap <= HPW && hv(tap - 1);
     // halo pixel of fragment row r = RM·wm + 4·rg + i, lane fr: hp = (r + dy)·18 + dx + fr, whose
     // swizzle term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or rg (RM·18, 72 ≡ 0 mod 8)
     const int xb = fr + dx + 2 * dy;
 #pragma unroll
     for (int ph = 0; ph < NPH; ++ph) {
       const int rg = NPH == 4 ? ph >> 1 : ph;
-      // ---- LOAD(NPH·u + ph): fragment reads, then waits / DMA
+      // ---- LOAD(NPH·u + ph): [normalise a landed halo piece], fragment reads, then waits / DMA
+      // piece normalised in this phase's MFMA segment (NPH 2: half 0 of piece tap-2 in phase 1,
+      // half 1 of piece tap-3 in phase 0; NPH 1: both halves of piece tap-2)
+      const int xe = NPH == 2 && ph == 0 ? tap - 3 : tap - 2;
+      const bool xf = GN && xe >= 0 && xe < HPW && cb + 1 < ncb && hv(xe);
 #pragma unroll
       for (int q = 0; q < NKH; ++q) {
         const int kh = NPH == 4 ? (ph & 1) : q;
@@ -848,7 +926,13 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
             acc[rg * 4 + i][j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[q][i], acc[rg * 4 + i][j], 0, 0, 0);
       }
+      if (xf) {  // after this wave's MFMAs (interleaved between them, or with its operands read
+                 // in the load segment, it measured slower: tools/kbench.py gnconv)
+        if (NPH == 1 || ph == 1) xform(cb + 1, xe, 0);
+        if (NPH == 1 || ph == 0) xform(cb + 1, xe, 1);
+      }
       __builtin_amdgcn_s_setprio(0);
+      if (xf) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // normalised values written
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -955,7 +1039,31 @@ bool vec_ok(const GemmP& p) {
   return ok;
 }
 
+// Halo engine (RDMI_CONV_HALO, read per launch for A/B measurements: 0 disables it, 1 = the
+// 4-phase variant where one exists, unset/2 = default).
+int halo_mode() {
+  const char* he = getenv("RDMI_CONV_HALO");
+  return he ? atoi(he) : 2;
+}
+
+// 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 output patches,
+// Cout % 256 == 0 or 128, no per-image row bias.
+bool halo_eligible(const rdmi_conv_args* a, int hmode) {
+  return hmode != 0 && a->kh == 3 && a->kw == 3 && a->Cin % 64 == 0 && a->stride == 1 && a->pad_top == 1 &&
+         a->pad_left == 1 && a->Ho % 16 == 0 && a->Wo % 16 == 0 && (a->Cout % 256 == 0 || a->Cout == 128) &&
+         !a->rowbias && a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
+}
+
+// input GroupNorm: groups divide Cin, the LDS scale/shift table holds ≤ 1024 channels
+bool in_gn_ok(const rdmi_conv_args* a) {
+  return a->in_groups > 0 && a->Cin <= 1024 && a->Cin % a->in_groups == 0;
+}
+
 }  // namespace
+
+extern "C" int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* a) {
+  return a && halo_eligible(a, halo_mode()) && in_gn_ok(a) ? 1 : 0;
+}
 
 extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   RDMI_REQUIRE(a && a->A && a->W && a->C, RDMI_E_ARG, "gemm: null pointer");
@@ -1021,38 +1129,45 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
                RDMI_E_ARG, "conv2d: GroupNorm moments need vector output, Cout %% 4 == 0, B*Ho*Wo %% 32 == 0");
   p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 2);
   p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 2);
-  // halo engine: 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 patches,
-  // Cout % 256 == 0 or 128 (RDMI_CONV_HALO: 0 disables it, 1 = the 4-phase variant; A/B measurements)
-  const char* he = getenv("RDMI_CONV_HALO");
-  const int hmode = he ? atoi(he) : 2;
-  const bool halo_ok = hmode != 0 && p.cmaj && a->stride == 1 && a->pad_top == 1 && a->pad_left == 1 &&
-                       a->Ho % 16 == 0 && a->Wo % 16 == 0 && (a->Cout % 256 == 0 || a->Cout == 128) && !p.rowbias &&
-                       a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
-  if (halo_ok) {
+  const int hmode = halo_mode();
+  RDMI_REQUIRE(!a->in_mean_rstd || (a->in_gamma && a->in_beta), RDMI_E_ARG, "conv2d: input GroupNorm needs gamma and beta");
+  RDMI_REQUIRE(!a->in_mean_rstd || (halo_eligible(a, hmode) && in_gn_ok(a)), RDMI_E_UNSUPPORTED,
+               "conv2d: input GroupNorm not supported for this shape (rdmi_conv2d_in_gn_supported)");
+  if (halo_eligible(a, hmode)) {
     const char* gm = getenv("RDMI_GEMM_GROUP");
     p.group_m = gm ? atoi(gm) : 8;
+    p.gmr = a->in_mean_rstd; p.ggam = a->in_gamma; p.gbet = a->in_beta; p.gG = a->in_groups; p.gsilu = a->in_silu;
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
+    const bool gn = p.gmr != nullptr;
     if (a->Cout % 256 == 0) {
       dim3 g(a->Cout / 256, patches, 1);
-      const bool ph2 = hmode != 1;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
+      const bool ph2 = hmode != 1 || gn;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
+#define RDMI_HALO(M, P, WN)                                                     \
+  do {                                                                          \
+    if (gn)                                                                     \
+      hipLaunchKernelGGL((conv_halo_kernel<M, P, WN, true>), g, dim3(512), 0, st, p);  \
+    else                                                                        \
+      hipLaunchKernelGGL((conv_halo_kernel<M, P, WN, false>), g, dim3(512), 0, st, p); \
+  } while (0)
       if (a->upsample) {
         if (ph2)
-          hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4>), g, dim3(512), 0, st, p);
+          RDMI_HALO(2, 2, 4);
         else
-          hipLaunchKernelGGL((conv_halo_kernel<2, 4, 4>), g, dim3(512), 0, st, p);
+          hipLaunchKernelGGL((conv_halo_kernel<2, 4, 4, false>), g, dim3(512), 0, st, p);
       } else {
         if (ph2)
-          hipLaunchKernelGGL((conv_halo_kernel<1, 2, 4>), g, dim3(512), 0, st, p);
+          RDMI_HALO(1, 2, 4);
         else
-          hipLaunchKernelGGL((conv_halo_kernel<1, 4, 4>), g, dim3(512), 0, st, p);
+          hipLaunchKernelGGL((conv_halo_kernel<1, 4, 4, false>), g, dim3(512), 0, st, p);
       }
     } else {
       dim3 g(1, patches, 1);
       if (a->upsample)
-        hipLaunchKernelGGL((conv_halo_kernel<2, 1, 2>), g, dim3(512), 0, st, p);
+        RDMI_HALO(2, 1, 2);
       else
-        hipLaunchKernelGGL((conv_halo_kernel<1, 1, 2>), g, dim3(512), 0, st, p);
+        RDMI_HALO(1, 1, 2);
+#undef RDMI_HALO
     }
     return rdmi::check_launch("conv2d halo");
   }

@@ -201,22 +201,48 @@ def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, 
     return g
 
 
+def _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn):
+    B, H, W, Cin = x.shape
+    pt = pad if pad_tl is None else pad_tl
+    a = _N.ConvArgs()
+    a.x, a.w = x.data_ptr(), w.data_ptr()
+    a.y = out.data_ptr() if out is not None else None
+    a.bias, a.residual, a.rowbias = _p(bias), _p(residual), _p(rowbias)
+    a.B, a.H, a.W, a.Cin, a.Cout, a.kh, a.kw = B, H, W, Cin, cout, k, k
+    a.stride, a.pad_top, a.pad_left, a.upsample, a.Ho, a.Wo = stride, pt, pt, int(upsample), Ho, Wo
+    a.Kp = w.shape[1]
+    a.y_ld = out.stride(-2) if out is not None else 0
+    a.res_ld = residual.stride(-2) if residual is not None else 0
+    a.alpha = alpha
+    a.rowbias_ld = 0 if (rowbias is None or rowbias.dim() == 1) else rowbias.stride(0)
+    if in_gn is not None:
+        mr, gamma, beta, groups, silu = in_gn
+        a.in_mean_rstd, a.in_gamma, a.in_beta = _p(mr), _p(gamma), _p(beta)
+        a.in_groups, a.in_silu = groups, int(silu)
+    return a
+
+
+def _out_hw(H, W, k, stride, pad, upsample, out_hw):
+    Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
+    if out_hw is None:
+        out_hw = ((Hi + 2 * pad - k) // stride + 1, (Wi + 2 * pad - k) // stride + 1)
+    return out_hw
+
+
 def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1, pad: int = 1,
            pad_tl: Optional[int] = None, upsample: bool = False, bias: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, rowbias: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, alpha: float = 1.0, out_hw=None, gn: bool = False,
-           _gn_slot=None) -> torch.Tensor:
+           in_gn=None, _gn_slot=None) -> torch.Tensor:
     """NHWC f16 conv.  x [B, H, W, Cin_pad]; w packed by pack_conv.  `pad` is symmetric; pad_tl
     overrides the top/left padding with bottom/right implied by out_hw (VAE Downsample2D).
-    gn=True: also emit the output's GroupNorm moments (as gemm)."""
+    gn=True: also emit the output's GroupNorm moments (as gemm).
+    in_gn=(mean_rstd, gamma, beta, groups, silu): GroupNorm(+SiLU) of x applied as it is read
+    (rdmi.h rdmi_conv_args.in_*; only where conv2d_in_gn_supported)."""
     _need(x, F16, "conv2d.x")
     _need(w, F16, "conv2d.w")
     B, H, W, Cin = x.shape
-    Hi, Wi = (2 * H, 2 * W) if upsample else (H, W)
-    pt = pad if pad_tl is None else pad_tl
-    if out_hw is None:
-        out_hw = ((Hi + 2 * pad - k) // stride + 1, (Wi + 2 * pad - k) // stride + 1)
-    Ho, Wo = out_hw
+    Ho, Wo = _out_hw(H, W, k, stride, pad, upsample, out_hw)
     if out is None:
         out = torch.empty((B, Ho, Wo, cout), dtype=F16, device=x.device)
     part = _gn_part(out, B * Ho * Wo, cout) if gn and _gn_slot is None else None
@@ -229,34 +255,57 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
                 slot = (part.data_ptr() + (s0 * Ho * Wo // 32) * 2 * 4, part.stride(0))
             elif part is not None:
                 part = None
+            ig = None
+            if in_gn is not None:
+                mr, gamma, beta, groups, silu = in_gn
+                ig = (mr[s0 * groups * 2:s1 * groups * 2], gamma, beta, groups, silu)
             conv2d(x[s0:s1], w, cout, k, stride, pad, pad_tl, upsample, bias,
                    None if residual is None else residual[s0:s1],
                    rb if rb is not None or rowbias is None else rowbias[s0:s1],
-                   out[s0:s1], alpha, out_hw, _gn_slot=slot)
+                   out[s0:s1], alpha, out_hw, in_gn=ig, _gn_slot=slot)
         _gn_attach(out, part)
         return out
-    a = _N.ConvArgs()
-    a.x, a.w, a.y = x.data_ptr(), w.data_ptr(), out.data_ptr()
-    a.bias, a.residual, a.rowbias = _p(bias), _p(residual), _p(rowbias)
-    a.B, a.H, a.W, a.Cin, a.Cout, a.kh, a.kw = B, H, W, Cin, cout, k, k
-    a.stride, a.pad_top, a.pad_left, a.upsample, a.Ho, a.Wo = stride, pt, pt, int(upsample), Ho, Wo
-    a.Kp = w.shape[1]
-    a.y_ld = out.stride(-2)
-    a.res_ld = residual.stride(-2) if residual is not None else 0
-    a.alpha = alpha
-    a.rowbias_ld = 0 if (rowbias is not None and rowbias.dim() == 1) else (rowbias.stride(0) if rowbias is not None else 0)
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
+    a = _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn)
     if part is not None:
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
         a.gn_part, a.gn_ld = _gn_slot
     with _Timed("implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin,
-                f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}"):
+                f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}"):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
     if _gn_slot is None:
         _gn_attach(out, part)
     return out
+
+
+def conv2d_in_gn_supported(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, groups: int, stride: int = 1,
+                           pad: int = 1, upsample: bool = False, rowbias=None, out_hw=None) -> bool:
+    """Whether rdmi_conv2d fuses an input GroupNorm for this conv (rdmi_conv2d_in_gn_supported)."""
+    B, H, W, Cin = x.shape
+    Ho, Wo = _out_hw(H, W, k, stride, pad, upsample, out_hw)
+    a = _conv_args(x, w, cout, k, stride, pad, None, upsample, None, None, rowbias, None, 1.0, Ho, Wo,
+                   (None, None, None, groups, 0))
+    return bool(lib.rdmi_conv2d_in_gn_supported(C.byref(a)))
+
+
+def gn_conv2d(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float, silu: bool,
+              w: torch.Tensor, cout: int, k: int, **conv_kw) -> torch.Tensor:
+    """conv2d(silu?(GroupNorm(x))): the norm fused into the conv's input path where the halo
+    engine runs it and it pays, else groupnorm then conv2d (identical values either way).
+    Policy (RDMI_GN_FUSE; tools/kbench.py gnconv on MI355X): 1 (default) fuses for Cin ≤ 256 —
+    the 768²/384² VAE convs, −6…10 % against apply + conv — but not for 512 channels, where the
+    in-conv normalisation costs more than the apply pass it saves (+3…11 %); 2 fuses wherever
+    supported; 0 never."""
+    mode = os.environ.get("RDMI_GN_FUSE", "1")
+    if mode != "0" and (mode == "2" or x.shape[-1] <= 256) and conv2d_in_gn_supported(
+            x, w, cout, k, groups, conv_kw.get("stride", 1), conv_kw.get("pad", 1), conv_kw.get("upsample", False),
+            conv_kw.get("rowbias"), conv_kw.get("out_hw")):
+        mr = groupnorm_stats(x, groups, eps)
+        return conv2d(x, w, cout, k, in_gn=(mr, gamma, beta, groups, silu), **conv_kw)
+    h = groupnorm(x, gamma, beta, groups, eps, silu)
+    return conv2d(h, w, cout, k, **conv_kw)
 
 
 # ----------------------------------------------------------------------------- norms

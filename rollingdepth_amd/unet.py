@@ -64,6 +64,11 @@ class _Conv:
                         upsample=upsample, bias=self.b, residual=residual, rowbias=rowbias, out=out, out_hw=out_hw,
                         gn=gn)
 
+    def normed(self, x, norm, groups, eps, silu=True, residual=None, rowbias=None, gn=False):
+        """self(silu?(GroupNorm(x))), the norm fused into the conv's input path where supported."""
+        return K.gn_conv2d(x, norm.g, norm.b, groups, eps, silu, self.w, self.cout, self.k, stride=self.stride,
+                           pad=self.pad, bias=self.b, residual=residual, rowbias=rowbias, gn=gn)
+
 
 class _Norm:
     def __init__(self, sd, key, dev):
@@ -84,15 +89,13 @@ class Resnet:
         self.temb_slot = temb_slot  # (offset, width) into the concatenated time projections
 
     def __call__(self, x, temb_all=None):
-        h = K.groupnorm(x, self.n1.g, self.n1.b, self.groups, self.eps, silu=True)
         rb = None
         if self.temb_slot is not None and temb_all is not None:
             o, w = self.temb_slot
             rb = temb_all[o:o + w]
-        h = self.c1(h, rowbias=rb, gn=True)
-        h = K.groupnorm(h, self.n2.g, self.n2.b, self.groups, self.eps, silu=True)
+        h = self.c1.normed(x, self.n1, self.groups, self.eps, rowbias=rb, gn=True)
         res = self.sc(x) if self.sc is not None else x
-        return self.c2(h, residual=res, gn=True)
+        return self.c2.normed(h, self.n2, self.groups, self.eps, residual=res, gn=True)
 
 
 class Transformer:

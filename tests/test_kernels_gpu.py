@@ -185,6 +185,55 @@ def test_groupnorm_moments_from_gemm(engine):
     assert (out.float() - ref).abs().max().item() < 1e-2
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,up,silu,G", [
+    (2, 32, 48, 128, 256, False, True, 32), (1, 16, 16, 512, 512, False, True, 32), (2, 8, 16, 256, 256, True, True, 32),
+    (2, 32, 16, 128, 128, False, True, 32), (1, 16, 8, 256, 128, True, False, 32), (3, 16, 32, 320, 256, False, True, 32),
+    (1, 16, 16, 1024, 256, False, True, 16), (2, 16, 16, 64, 128, False, True, 8)])
+def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G):
+    """GroupNorm(+SiLU) applied inside the halo conv's input path (rdmi_conv_args.in_*) against the
+    unfused groupnorm → conv2d pair on the same data: the same normalised f16 values feed the same
+    MFMA order, so the outputs agree bitwise; plus an fp32 torch reference.  Images get distinct
+    statistics (per-image scale/offset) so a wrong image index would show."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(21)
+    scale = torch.arange(1, B + 1, device=DEV).view(B, 1, 1, 1) * 0.7
+    x = (torch.randn(B, H, W, Cin, device=DEV, generator=g) * scale + scale).half()
+    w = torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9)
+    wp = K_.pack_conv(w, DEV)
+    b = torch.randn(Cout, device=DEV, generator=g)
+    gm = 1 + 0.2 * torch.randn(Cin, device=DEV, generator=g)
+    bt = 0.2 * torch.randn(Cin, device=DEV, generator=g)
+    assert K_.conv2d_in_gn_supported(x, wp, Cout, 3, G, upsample=up)
+    mr = K_.groupnorm_stats(x, G, 1e-6)
+    y = K_.conv2d(x, wp, Cout, 3, upsample=up, bias=b, in_gn=(mr, gm, bt, G, silu))
+    h = K_.groupnorm(x, gm, bt, G, 1e-6, silu)
+    y_ref = K_.conv2d(h, wp, Cout, 3, upsample=up, bias=b)
+    assert torch.equal(y, y_ref)
+    hf = F.group_norm(x.float().permute(0, 3, 1, 2), G, gm, bt, 1e-6)
+    hf = F.silu(hf) if silu else hf
+    hf = F.interpolate(hf, scale_factor=2.0, mode="nearest") if up else hf
+    ref = F.conv2d(hf, w.to(DEV), b, padding=1)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
+    # the helper picks the fused path and matches as well
+    y2 = K_.gn_conv2d(x, gm, bt, G, 1e-6, silu, wp, Cout, 3, upsample=up, bias=b)
+    assert torch.equal(y2, y_ref)
+
+
+def test_conv2d_fused_input_groupnorm_unsupported():
+    """Shapes outside the halo engine refuse an input GroupNorm loudly; gn_conv2d falls back to the
+    unfused pair."""
+    K_ = _k()
+    x = torch.randn(1, 12, 12, 64, device=DEV).half()
+    wp = K_.pack_conv(torch.randn(64, 64, 3, 3) / 24, DEV)
+    gm, bt = torch.ones(64, device=DEV), torch.zeros(64, device=DEV)
+    assert not K_.conv2d_in_gn_supported(x, wp, 64, 3, 32)
+    mr = K_.groupnorm_stats(x, 32, 1e-6)
+    with pytest.raises(RuntimeError):
+        K_.conv2d(x, wp, 64, 3, in_gn=(mr, gm, bt, 32, True))
+    y = K_.gn_conv2d(x, gm, bt, 32, 1e-6, True, wp, 64, 3)
+    assert torch.equal(y, K_.conv2d(K_.groupnorm(x, gm, bt, 32, 1e-6, True), wp, 64, 3))
+
+
 @pytest.mark.parametrize("B,H,W,C,silu", [(2, 24, 20, 128, True), (1, 7, 9, 64, False), (3, 33, 17, 128, True)])
 def test_conv3x3_to1_gn(B, H, W, C, silu):
     """Fused decoder head (convhead.hip) vs GroupNorm(+SiLU) → conv2d(pad 1) to one channel in fp32."""

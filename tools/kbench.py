@@ -55,6 +55,32 @@ def bench_conv(iters):
         print(f"conv  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
 
+def bench_gnconv(iters):
+    """GroupNorm+SiLU → conv: apply pass + conv vs the norm fused into the halo conv's input."""
+    from rollingdepth_amd._native import lib
+    for lab, B, H, W, ci, co, up in conv_cases()[5:]:
+        x = torch.randn(B, H, W, ci, device="cuda").half()
+        w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
+        g, b = torch.ones(ci, device="cuda"), torch.zeros(ci, device="cuda")
+        Ho, Wo = (2 * H, 2 * W) if up else (H, W)
+        out = torch.empty(B, Ho, Wo, co, device="cuda", dtype=torch.float16)
+        h = torch.empty_like(x)
+        mr = K.groupnorm_stats(x, 32, 1e-6)
+        if not K.conv2d_in_gn_supported(x, w, co, 3, 32, upsample=up):
+            continue
+
+        def unfused():
+            lib.rdmi_groupnorm_apply(x.data_ptr(), h.data_ptr(), B, H * W, ci, 32, mr.data_ptr(), g.data_ptr(),
+                                     b.data_ptr(), 1, K._stream())
+            K.conv2d(h, w, co, 3, upsample=up, out=out)
+
+        ms_u = timeit(unfused, iters)
+        ms_f = timeit(lambda: K.conv2d(x, w, co, 3, upsample=up, out=out, in_gn=(mr, g, b, 32, True)), iters)
+        fl = 2.0 * B * Ho * Wo * co * ci * 9
+        print(f"gnconv {lab:31s} apply+conv {ms_u * 1e3:9.1f} us | fused {ms_f * 1e3:9.1f} us "
+              f"{fl / ms_f / 1e9:8.1f} TFLOP/s")
+
+
 def bench_gemm(iters):
     for lab, M, N, Kd, geglu in [("L0 qkv 221k x 960 x 320", 221184, 960, 320, False),
                                  ("L0 ff1 geglu 221k x 2560 x 320", 221184, 2560, 320, True),
@@ -148,4 +174,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
