@@ -148,7 +148,9 @@ int rdmi_attention_smallkv(const void* q, const void* k, const void* v, void* o,
 
 /* Row softmax: p[r, :] = softmax(scale * s[r, :]) (f32 in, f16 out).  Used with two rdmi_gemm
  * calls for the single-head d=C VAE mid-block attention (unet_2d_blocks.py:680-697). */
-int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, float scale, void* stream);
+/* p[r·p_ld + c] = softmax_c(scale·s[r·cols + c]) for c < cols, 0 for cols ≤ c < p_ld (so a PV GEMM
+ * can run on K = p_ld, a multiple of 8, when the key count is not). */
+int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Layout / elementwise helpers (f16 NHWC unless stated)
@@ -163,6 +165,11 @@ int rdmi_nhwc_to_nchw_f32(const void* x, long ld, float* y, int B, int C, int H,
                           float scale, float shift, void* stream);
 /* y[p, 0:Ca] = a[p, :], y[p, Ca:Ca+Cb] = b[p, :]  (torch.cat dim=1 of CrossAttn/UpBlock skips) */
 int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, void* stream);
+/* NHWC f16 nearest resize to an explicit size: y[b,yo,xo] = x[b, ⌊yo·H/Ho⌋, ⌊xo·W/Wo⌋] (f32 scale,
+ * clamped) — F.interpolate(size=…, mode="nearest") of Upsample2D when the UNet forwards an
+ * upsample size (latent not a multiple of 2^levels; unet_2d_condition.py forward_upsample_size,
+ * upsampling.py:167-178).  C % 8 == 0. */
+int rdmi_resize_nearest(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo, void* stream);
 /* 2-D transpose per batch: dst[b][c][r] = src[b][r][c] (f16) */
 int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, long src_ld,
                    long dst_ld, void* stream);

@@ -121,9 +121,7 @@ class CrossFrameAttnProcessor:
                 raise NotImplementedError(f"head_dim {D} with {H} heads")
             kk = k if k.shape[0] == B else k.expand(B, -1, -1).contiguous()
             vv = v if v.shape[0] == B else v.expand(B, -1, -1).contiguous()
-            s = K.gemm(q, kk, D, out_f32=True)
-            pr = K.softmax_rows(s, 1.0 / math.sqrt(D))
-            o = K.gemm(pr, K.transpose(vv), kk.shape[1])
+            o = K.attention_1head(q, kk, vv, 1.0 / math.sqrt(D))
         res_tok = None
         if attn.residual_connection and input_ndim == 3 and num_view is None:
             res_tok = residual.to(F16).reshape(B * S, C).contiguous()

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void attn_smallkv(const f16* __restrict__ q, c
 }
 
 __global__ __launch_bounds__(256) void softmax_rows_k(const float* __restrict__ s, f16* __restrict__ pout, long cols,
-                                                      float scale) {
+                                                      long p_ld, float scale) {
   const long row = blockIdx.x;
   const float* sr = s + row * cols;
   __shared__ float red[4];
@@ -375,8 +375,9 @@ __global__ __launch_bounds__(256) void softmax_rows_k(const float* __restrict__ 
   __syncthreads();
   sum = red[0] + red[1] + red[2] + red[3];
   const float inv = 1.f / sum;
-  f16* pr = pout + row * cols;
+  f16* pr = pout + row * p_ld;
   for (long c = threadIdx.x; c < cols; c += 256) pr[c] = (f16)(__expf((sr[c] - mx) * scale) * inv);
+  for (long c = cols + threadIdx.x; c < p_ld; c += 256) pr[c] = (f16)0.f;  // K padding of the PV GEMM
 }
 
 }  // namespace
@@ -409,8 +410,9 @@ extern "C" int rdmi_attention_smallkv(const void* q, const void* k, const void* 
   return rdmi::check_launch("attention_smallkv");
 }
 
-extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, float scale, void* stream) {
-  RDMI_REQUIRE(s && p && rows > 0 && cols > 0, RDMI_E_ARG, "softmax_rows: bad args");
-  hipLaunchKernelGGL(softmax_rows_k, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, s, (f16*)p, cols, scale);
+extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, void* stream) {
+  RDMI_REQUIRE(s && p && rows > 0 && cols > 0 && p_ld >= cols, RDMI_E_ARG, "softmax_rows: bad args");
+  hipLaunchKernelGGL(softmax_rows_k, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, s, (f16*)p, cols, p_ld,
+                     scale);
   return rdmi::check_launch("softmax_rows");
 }

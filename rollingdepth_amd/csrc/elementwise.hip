@@ -49,6 +49,23 @@ __global__ void concat_k(const f16* __restrict__ a, int Ca, const f16* __restric
   }
 }
 
+// nearest resize, PyTorch's index rule for an explicit output size: src = min(floor(dst·(in/out)), in−1)
+// with the scale in f32 (F.interpolate(mode="nearest", size=...), as Upsample2D uses it)
+__global__ void resize_nearest_k(const f16* __restrict__ x, int H, int W, int CV, f16* __restrict__ y, int Ho, int Wo,
+                                 long n) {
+  const float sy = (float)H / (float)Ho, sx = (float)W / (float)Wo;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    const long px = i / CV;
+    const int xo = (int)(px % Wo);
+    const long r = px / Wo;
+    const int yo = (int)(r % Ho);
+    const long b = r / Ho;
+    const int yi = min((int)floorf((float)yo * sy), H - 1), xi = min((int)floorf((float)xo * sx), W - 1);
+    ((f16x8*)y)[i] = ((const f16x8*)x)[((b * H + yi) * W + xi) * CV + cv];
+  }
+}
+
 __global__ void transpose_k(const f16* __restrict__ src, f16* __restrict__ dst, long rows, long cols, long sld,
                             long dld) {
   __shared__ f16 tile[64][65];
@@ -198,6 +215,15 @@ extern "C" int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb
   hipLaunchKernelGGL(concat_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)a, Ca, (const f16*)b,
                      Cb, (f16*)y, P);
   return rdmi::check_launch("concat");
+}
+
+extern "C" int rdmi_resize_nearest(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo, void* stream) {
+  RDMI_REQUIRE(x && y && B > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, RDMI_E_ARG, "resize_nearest: bad args");
+  RDMI_REQUIRE(C % 8 == 0, RDMI_E_ALIGN, "resize_nearest: C (%d) must be a multiple of 8", C);
+  const long n = (long)B * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(resize_nearest_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, H, W, C / 8,
+                     (f16*)y, Ho, Wo, n);
+  return rdmi::check_launch("resize_nearest");
 }
 
 extern "C" int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, long src_ld, long dst_ld,

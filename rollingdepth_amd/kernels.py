@@ -421,12 +421,32 @@ def attention_smallkv(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: 
 
 
 def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """f32 scores [..., cols] → f16 probabilities; `out` may be wider (row stride p_ld ≥ cols: the
+    extra columns are written as zeros)."""
     _need(s, F32, "softmax_rows.s")
     cols = s.shape[-1]
     rows = s.numel() // cols
     out = torch.empty(s.shape, dtype=F16, device=s.device) if out is None else out
-    check(lib.rdmi_softmax_rows(s.data_ptr(), out.data_ptr(), rows, cols, scale, _stream()), "rdmi_softmax_rows")
+    p_ld = out.shape[-1]
+    if out.numel() != rows * p_ld or not out.is_contiguous() or p_ld < cols:
+        raise ValueError("softmax_rows: out must be a contiguous [..., >= cols] tensor")
+    check(lib.rdmi_softmax_rows(s.data_ptr(), out.data_ptr(), rows, cols, p_ld, scale, _stream()), "rdmi_softmax_rows")
     return out
+
+
+def attention_1head(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:
+    """Single-head attention for any head dim (the VAE mid-block, d = C): f32 scores GEMM → row
+    softmax → PV GEMM.  q [B, Sq, D], k/v [B, Sk, D] (row strides any, 16-B aligned) → [B, Sq, D].
+    A key count that is not a multiple of 8 runs the PV GEMM on K padded with zero probabilities."""
+    B, Sq, D = q.shape
+    Sk = k.shape[1]
+    s = gemm(q, k, D, out_f32=True)
+    Sp = (Sk + 7) // 8 * 8
+    p = softmax_rows(s, scale, out=torch.empty((B, Sq, Sp), dtype=F16, device=q.device))
+    del s
+    vt = torch.zeros((B, D, Sp), dtype=F16, device=q.device) if Sp != Sk else None
+    vt = transpose(v, out=vt)
+    return gemm(p, vt, Sp)
 
 
 def transpose(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -469,6 +489,17 @@ def concat_channels(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor
     P = a.numel() // Ca
     out = torch.empty((*a.shape[:-1], Ca + Cb), dtype=F16, device=a.device) if out is None else out
     check(lib.rdmi_concat_channels(a.data_ptr(), Ca, b.data_ptr(), Cb, out.data_ptr(), P, _stream()), "rdmi_concat")
+    return out
+
+
+def resize_nearest(x: torch.Tensor, size, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NHWC f16 [B, H, W, C] → [B, Ho, Wo, C], F.interpolate(size=(Ho, Wo), mode="nearest")."""
+    _need(x, F16, "resize_nearest.x")
+    B, H, W, C_ = x.shape
+    Ho, Wo = size
+    out = torch.empty((B, Ho, Wo, C_), dtype=F16, device=x.device) if out is None else out
+    check(lib.rdmi_resize_nearest(x.data_ptr(), B, H, W, C_, out.data_ptr(), Ho, Wo, _stream()),
+          "rdmi_resize_nearest")
     return out
 
 

@@ -175,8 +175,8 @@ class RollingDepthPipeline:
     def encode_rgb(self, frames_nchw: torch.Tensor) -> torch.Tensor:
         """[N,3,H,W] in [-1,1] (any float dtype, on device) → NHWC f16 [N, h, w, 8] latents·0.18215."""
         N, _, H, W = frames_nchw.shape
-        f = self.vae.factor
-        out = torch.zeros((N, H // f, W // f, self.vae.lat_pad), dtype=F16, device=self.device)
+        h, w = self.vae.latent_hw(H, W)
+        out = torch.zeros((N, h, w, self.vae.lat_pad), dtype=F16, device=self.device)
         for i in range(0, N, self.vae_batch):
             x = K.nchw_to_nhwc(frames_nchw[i:i + self.vae_batch], self.vae.in_pad)
             self.vae.encode(x, out=out[i:i + self.vae_batch])

@@ -252,9 +252,6 @@ class UNet:
         """sample: NHWC f16 [B, h, w, in_ch_pad]; one timestep value for the whole batch (the
         pipeline repeats a scalar t, rollingdepth_pipeline.py:434).  Returns NHWC [B, h, w, out]."""
         B, h, w, _ = sample.shape
-        f = 2 ** (len(self.ch) - 1)
-        if h % f or w % f:
-            raise NotImplementedError(f"latent {h}x{w} not a multiple of {f} (forward_upsample_size path)")
         temb = self.time_embedding(t)
         x = self.conv_in(sample, gn=True)
         skips = [x]
@@ -277,6 +274,12 @@ class UNet:
                 if blk["attn"]:
                     x = blk["attn"][j](x, num_view)
             if blk["us"] is not None:
-                x = blk["us"](x, upsample=True, gn=True)
+                # forward_upsample_size (unet_2d_condition.py): a latent that is not a multiple of
+                # 2^levels upsamples to the next skip's size, not ×2 (Upsample2D with output_size)
+                size = tuple(skips[-1].shape[1:3])
+                if size == (2 * x.shape[1], 2 * x.shape[2]):
+                    x = blk["us"](x, upsample=True, gn=True)
+                else:
+                    x = blk["us"](K.resize_nearest(x, size), gn=True)
         x = K.groupnorm(x, self.norm_out.g, self.norm_out.b, self.groups, self.eps, silu=True)
         return self.conv_out(x)

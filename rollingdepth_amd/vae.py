@@ -53,11 +53,7 @@ class VaeAttention:
         t = K.groupnorm(x, self.norm.g, self.norm.b, self.groups, 1e-6, silu=False)
         qkv = K.gemm(t.view(B * S, C), self.qkv_w, C, bias=self.qkv_b).view(B, S, 3 * C)
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
-        s = K.gemm(q, k, C, out_f32=True)
-        p = K.softmax_rows(s, 1.0 / math.sqrt(C))
-        del s
-        vt = K.transpose(v)
-        o = K.gemm(p, vt, S)
+        o = K.attention_1head(q, k, v, 1.0 / math.sqrt(C))
         out = self.out(o.view(B * S, C), residual=x.view(B * S, C), gn=True)
         return K.gn_view(out, (B, H, W, C))
 
@@ -117,19 +113,28 @@ class VAE:
         self.groups = g
 
     # ------------------------------------------------------------------ encode
+    @staticmethod
+    def _down(H: int, W: int):
+        """Downsample2D(padding=0) output size: F.pad(0,1,0,1) then 3×3 stride 2, ⌊(H+1−3)/2⌋+1."""
+        return (H - 2) // 2 + 1, (W - 2) // 2 + 1
+
+    def latent_hw(self, H: int, W: int):
+        """Latent size of an H×W frame (H/8 for multiples of 8; odd sizes round up per level)."""
+        for _ in range(len(self.cfg["block_out_channels"]) - 1):
+            H, W = self._down(H, W)
+        return H, W
+
     def encode(self, x: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         """x: NHWC f16 [B, H, W, in_pad] in [-1, 1] → scaled latent mean NHWC [B, h, w, lat_pad]
         (channels ≥ latent_channels are zero)."""
         B, H, W, _ = x.shape
-        if H % self.factor or W % self.factor:
-            raise NotImplementedError(f"frame {H}x{W} not a multiple of {self.factor}")
         h = self.e_in(x, gn=True)
         for res, ds in self.e_down:
             for r in res:
                 h = r(h)
             if ds is not None:
                 # Downsample2D(padding=0): F.pad(0,1,0,1) then 3×3 s2 (downsampling.py:141-146)
-                h = ds(h, pad_tl=0, out_hw=(h.shape[1] // 2, h.shape[2] // 2), gn=True)
+                h = ds(h, pad_tl=0, out_hw=self._down(h.shape[1], h.shape[2]), gn=True)
         h = self.e_mid[0](h)
         h = self.e_attn(h)
         h = self.e_mid[1](h)

@@ -348,20 +348,23 @@ def test_attention_smallkv():
     assert (o.float() - ref).abs().max().item() < 3e-3
 
 
-def test_vae_style_attention_via_gemm():
-    """GEMM(f32 scores) → softmax_rows → GEMM with Vᵀ, the d=C single-head path."""
+@pytest.mark.parametrize("S", [256, 234, 97])
+def test_vae_style_attention_via_gemm(S):
+    """GEMM(f32 scores) → softmax_rows → GEMM with Vᵀ, the d=C single-head path (attention_1head);
+    key counts that are not multiples of 8 run the PV GEMM on zero-padded K."""
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(10)
-    B, S, D = 2, 256, 128
+    B, D = 2, 128
     q = torch.randn(B, S, D, device=DEV, generator=g).half()
     k = torch.randn(B, S, D, device=DEV, generator=g).half()
     v = torch.randn(B, S, D, device=DEV, generator=g).half()
-    s = K_.gemm(q, k, D, out_f32=True)
-    p = K_.softmax_rows(s, 1.0 / math.sqrt(D))
-    vt = K_.transpose(v)
-    o = K_.gemm(p, vt, S)
+    o = K_.attention_1head(q, k, v, 1.0 / math.sqrt(D))
     ref = F.scaled_dot_product_attention(q.float()[:, None], k.float()[:, None], v.float()[:, None])[:, 0]
     assert (o.float() - ref).abs().max().item() < 5e-3
+    if S % 8 == 0:
+        s = K_.gemm(q, k, D, out_f32=True)
+        p = K_.softmax_rows(s, 1.0 / math.sqrt(D))
+        assert torch.equal(K_.gemm(p, K_.transpose(v), S), o)
 
 
 def test_layout_and_elementwise():
@@ -397,3 +400,14 @@ def test_layout_and_elementwise():
     ref = ref / ref.max()
     ref = ref * 2.0 - 1.0
     assert torch.equal(zr, ref)
+
+
+@pytest.mark.parametrize("H,W,Ho,Wo", [(7, 7, 13, 14), (14, 27, 27, 54), (12, 12, 24, 24), (5, 9, 11, 10)])
+def test_resize_nearest(H, W, Ho, Wo):
+    """rdmi_resize_nearest == F.interpolate(size=..., mode="nearest") bitwise (Upsample2D output_size)."""
+    K_ = _k()
+    x = torch.randn(2, H, W, 16, device=DEV).half()
+    y = K_.resize_nearest(x, (Ho, Wo))
+    ref = F.interpolate(x.permute(0, 3, 1, 2).float(), size=(Ho, Wo), mode="nearest").half().permute(0, 2, 3, 1)
+    assert torch.equal(y, ref)
+

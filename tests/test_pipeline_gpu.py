@@ -109,3 +109,36 @@ def test_sharded_forward_world1_equals_forward():
     for a, b in zip(per_d, out.snippet_ls):
         assert torch.equal(a.cpu(), b.view(a.shape))
     assert torch.equal(depth.cpu(), out.depth_pred)
+
+
+def test_non_multiple_latent_vs_oracle():
+    """A frame size whose latent is not a multiple of the UNet's 2^levels (and an odd pixel width):
+    the VAE's padded stride-2 downsamples round up, and the UNet upsamples to each skip's size
+    (forward_upsample_size, unet_2d_condition.py; Upsample2D output_size) — against the CPU
+    oracle on the same synthetic weights and inputs (this size has no reference golden: the
+    oracle's upsample path is the one pinned by the golden fixtures at ×2 sizes)."""
+    from oracle import rd_oracle as O
+    from rollingdepth_amd import weights as W
+    from rollingdepth_amd.pipeline import RollingDepthPipeline
+
+    t = load_file(os.path.join(G, "tiny_pipeline.safetensors"))
+    meta = json.load(open(os.path.join(G, "tiny_pipeline.json")))
+    pipe = RollingDepthPipeline.from_synthetic(meta["unet"], meta["vae"], meta["scheduler"], device="cuda")
+    pipe.empty_text_embed = t["context"]
+    g = torch.Generator().manual_seed(7)
+    N, H, Wd = 7, 36, 27
+    frames = torch.rand(N, 3, H, Wd, generator=g) * 2 - 1
+    h, w = pipe.vae.latent_hw(H, Wd)
+    assert (h, w) == (18, 13)
+    noise = torch.randn(1, 4, h, w, generator=g)
+    out = pipe.forward(frames[None], [1, 2], True, [3], [1], [1], None, 0, 3, 6, None, False, 4, False,
+                       init_noise=noise)
+    usd = W.synth_state_dict(W.unet_param_shapes(meta["unet"]))
+    vsd = W.synth_state_dict(W.vae_param_shapes(meta["vae"]))
+    with torch.no_grad():
+        ref = O.pipeline_forward(usd, meta["unet"], vsd, meta["vae"], meta["scheduler"], frames, noise,
+                                 t["context"], [1, 2], True)
+    assert out.depth_pred.shape == ref.shape == (N, 1, 2 * h, 2 * w)
+    l1 = (out.depth_pred.float() - ref).abs().mean().item()
+    print(f"non-multiple latent {h}x{w}: depth L1 vs oracle {l1:.2e}")
+    assert l1 < 1e-2

@@ -81,6 +81,21 @@ def bench_gnconv(iters):
               f"{fl / ms_f / 1e9:8.1f} TFLOP/s")
 
 
+def bench_cinsweep(iters):
+    """Fixed tile count, growing K: time = per-tile fixed cost + per-K-tile cost (halo engine)."""
+    for co in (128, 256):
+        for ci in (64, 128, 256, 512):
+            B, H = 4, 768 if co == 128 else 384
+            x = torch.randn(B, H, H, ci, device="cuda").half()
+            w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
+            out = torch.empty(B, H, H, co, device="cuda", dtype=torch.float16)
+            ms = timeit(lambda: K.conv2d(x, w, co, 3, out=out), iters)
+            fl = 2.0 * B * H * H * co * ci * 9
+            tiles = B * H * H // 256 * (co // 128 if co == 128 else co // 256)
+            print(f"sweep {H}^2 x{B} {ci:4d}->{co:4d} {ms * 1e3:9.1f} us {fl / ms / 1e9:8.1f} TFLOP/s "
+                  f"{ms * 1e3 / (tiles / 256):7.2f} us per tile-round ({ci // 64 * 9} K-tiles)")
+
+
 def bench_gemm(iters):
     for lab, M, N, Kd, geglu in [("L0 qkv 221k x 960 x 320", 221184, 960, 320, False),
                                  ("L0 ff1 geglu 221k x 2560 x 320", 221184, 2560, 320, True),
@@ -174,4 +189,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
