@@ -944,6 +944,201 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq);
 }
 
+// Two-workgroups-per-CU halo conv for 128-channel output tiles (the VAE's 768² convs).  With
+// 128 output channels and Cin = 128 a tile has only 18 K-tiles, so the 8-wave single-workgroup
+// variant above pays its prologue and epilogue un-overlapped on every tile (≈7 µs of ≈27 µs:
+// tools/kbench.py sweep) and its 64×64 wave tiles read 0.5 KiB of LDS per MFMA.  Here a 4-wave
+// workgroup owns a 16×16 patch × 128 channels with 128-pixel × 64-channel wave tiles (0.375 KiB
+// per MFMA, as the 256-channel variant) and ≤ 80 KiB of LDS (one 41-KiB halo buffer, a 2-slot
+// 16-KiB weight ring, the GroupNorm table), so two workgroups share each CU and one's epilogue,
+// prologue and halo refills run under the other's MFMAs — occupancy, not an intra-workgroup
+// ping-pong, hides the latencies.  Per K-tile: wait for the own weight DMA of this K-tile
+// (issued one K-tile earlier) and the own fragment reads of the previous one, one barrier, issue
+// the next K-tile's weights into the other slot (last read in the previous K-tile), then 24
+// fragment reads and 64 MFMAs.  At a channel block's first tap the halo is refilled in place:
+// barrier (all reads of the previous block's halo done), DMA, wait, [GroupNorm+SiLU of the own
+// pieces], barrier.
+template <int MODE, bool GN>
+__global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
+  constexpr int BN = 128, BKP = 64, RM = 8, RN = 4;
+  constexpr int HWD = 18, HPIX = HWD * HWD;
+  constexpr int HPC = 41;                  // pieces of 8 halo pixels (41·8 = 328 >= 324)
+  constexpr int HPW = 11;                  // piece slots per wave (4 × 11 = 44 >= 41)
+  constexpr int HALO = HPC * 8 * BKP;      // halves (41 KiB)
+  constexpr int BSLOT = BN * BKP;          // halves (16 KiB)
+  constexpr int NB = 4;                    // weight pieces per wave per K-tile (16 / 4 waves)
+  constexpr int GNT = GN ? 256 : 0;        // sc[256], sh[256] floats (Cin <= 256)
+  __shared__ __attribute__((aligned(16))) f16 lds[HALO + 2 * BSLOT + 4 * GNT];
+  float* const gnt = (float*)(lds + HALO + 2 * BSLOT);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int wids = __builtin_amdgcn_readfirstlane(wid);
+  const int nbx = gridDim.x;
+  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+  int mt_, nt_;
+  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN;
+  const int pxn = p.Wo >> 4, pyn = p.Ho >> 4;
+  const int px = mt_ % pxn;
+  const int py = (mt_ / pxn) % pyn;
+  const int b = mt_ / (pxn * pyn);
+  const int y0 = py * 16, x0 = px * 16;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.Wt, (short)0, (int)p.w_bytes, 0x00020000);
+
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ lrow;
+  const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
+  int hoff[HPW];  // piece t = wid + 4e: halo pixels 8t + lrow
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    const int hp = (wid + 4 * e) * 8 + lrow;
+    const int hr = hp / HWD, hc = hp - hr * HWD;
+    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
+    const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
+    const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
+    hoff[e] = ok ? ((b * p.IH + sy) * p.IW + sx) * p.Cin : -1;
+  }
+  int brow[NB];
+#pragma unroll
+  for (int e = 0; e < NB; ++e) {
+    const int n = n0 + (wid + 4 * e) * 8 + lrow;
+    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+  }
+  const int ncb = p.Cin >> 6;
+  auto hv = [&](int e) { return wids + 4 * e < HPC; };
+  auto issueHalo = [&](int cb) {
+#pragma unroll
+    for (int e = 0; e < HPW; ++e)
+      if (hv(e)) {
+        f16* lh = lds + (wid + 4 * e) * 8 * BKP;
+        dma16(ra_, hoff[e] >= 0 ? (unsigned)(hoff[e] + cb * 64 + chunk * 8) * 2u : OOB, lh);
+      }
+  };
+  auto issueB = [&](int u) {
+    const int kk = u * BKP + chunk * 8;
+    const bool kok = kk < p.Kvalid;
+    f16* lb = lds + HALO + (u & 1) * BSLOT;
+#pragma unroll
+    for (int e = 0; e < NB; ++e) {
+      const bool ok = brow[e] >= 0 && kok;
+      dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 4 * e) * 8 * BKP);
+    }
+  };
+  // in-place GroupNorm (+SiLU) of this wave's landed pieces of the halo of channel block cb
+  auto xformHalo = [&](int cb) {
+    const float* ts = gnt + cb * 64 + chunk * 8;
+    const f32x4 s0 = *(const f32x4*)ts, s1 = *(const f32x4*)(ts + 4);
+    const f32x4 h0 = *(const f32x4*)(ts + GNT), h1 = *(const f32x4*)(ts + GNT + 4);
+    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+    const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+#pragma unroll
+    for (int e = 0; e < HPW; ++e)
+      if (hv(e)) {
+        f16* lh = lds + (wid + 4 * e) * 8 * BKP + lane * 8;
+        const f16x8 v = *(const f16x8*)lh;
+        const bool in = hoff[e] >= 0;
+        f16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float f = fmaf((float)v[i], sc[i], sh[i]);
+          if (p.gsilu) f = silu_f(f);
+          o[i] = in ? (f16)f : (f16)0.f;
+        }
+        *(f16x8*)lh = o;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = ncb * 9;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
+  const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+
+  // prologue: halo(0), B(0) [, GroupNorm scale/shift of image b]
+  issueHalo(0);
+  issueB(0);
+  if constexpr (GN) {
+    const int c = tid;
+    float mean = 0.f, rstd = 0.f, gm = 0.f, bt = 0.f;
+    if (c < p.Cin) {
+      const int g = c / (p.Cin / p.gG);
+      mean = p.gmr[2 * (b * p.gG + g)];
+      rstd = p.gmr[2 * (b * p.gG + g) + 1];
+      gm = p.ggam[c];
+      bt = p.gbet[c];
+    }
+    const float sc = rstd * gm;
+    gnt[c] = sc;
+    gnt[GNT + c] = bt - mean * sc;
+  }
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr (GN) {
+    xformHalo(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("" ::: "memory");
+
+  const int wms = __builtin_amdgcn_readfirstlane(wm);
+  for (int u = 0; u < nk; ++u) {
+    const int cb = u / 9;
+    const int tap = u - cb * 9;
+    const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+    if (u > 0) {
+      if (tap == 0) {  // refill the halo with channel block cb
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is past its reads of halo(cb-1)
+        asm volatile("" ::: "memory");
+        issueHalo(cb);
+        wait_vmcnt<0>();  // B(u) and the halo pieces of this wave
+        if constexpr (GN) xformHalo(cb);
+      } else {
+        wait_vmcnt<0>();  // B(u), issued one K-tile ago
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of B(u-1) done (slot reuse)
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (u + 1 < nk) issueB(u + 1);
+    const f16* lb = lds + HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
+    const int xb = fr + dx + 2 * dy;
+    f16x8 af[2][RM], bf[2][RN];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int off = kh ? off1 : off0;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const f16* row = lds + ((wms * RM + i + dy) * HWD + dx) * BKP;
+        af[kh][i] = *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
+      }
+    }
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
+  }
+  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq);
+}
+
 // Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
 // engine only, 2 = a ping-pong tile whenever the shape allows one, unset/1 = by estimated cost.
 int pp_mode() {
@@ -1040,23 +1235,28 @@ bool vec_ok(const GemmP& p) {
 }
 
 // Halo engine (RDMI_CONV_HALO, read per launch for A/B measurements: 0 disables it, 1 = the
-// 4-phase variant where one exists, unset/2 = default).
+// 4-phase variant where one exists, 3 = the two-workgroups-per-CU variant for every Cout % 128 ==
+// 0, 4 = the 8-wave variant for 128 output channels instead of the two-workgroups-per-CU one,
+// unset/2 = default).
 int halo_mode() {
   const char* he = getenv("RDMI_CONV_HALO");
   return he ? atoi(he) : 2;
 }
 
 // 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 output patches,
-// Cout % 256 == 0 or 128, no per-image row bias.
+// Cout % 64 == 0 (a ragged last 128-channel tile in the two-workgroups-per-CU variant), no
+// per-image row bias.
 bool halo_eligible(const rdmi_conv_args* a, int hmode) {
   return hmode != 0 && a->kh == 3 && a->kw == 3 && a->Cin % 64 == 0 && a->stride == 1 && a->pad_top == 1 &&
-         a->pad_left == 1 && a->Ho % 16 == 0 && a->Wo % 16 == 0 && (a->Cout % 256 == 0 || a->Cout == 128) &&
+         a->pad_left == 1 && a->Ho % 16 == 0 && a->Wo % 16 == 0 && a->Cout % 64 == 0 &&
          !a->rowbias && a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
 }
 
-// input GroupNorm: groups divide Cin, the LDS scale/shift table holds ≤ 1024 channels
+// input GroupNorm: groups divide Cin, the LDS scale/shift table holds ≤ 1024 channels (≤ 256 in
+// the two-workgroups-per-CU variant, the only one for Cout % 256 != 0 other than 128)
 bool in_gn_ok(const rdmi_conv_args* a) {
-  return a->in_groups > 0 && a->Cin <= 1024 && a->Cin % a->in_groups == 0;
+  const int cmax = (a->Cout % 256 == 0 || a->Cout == 128) ? 1024 : 256;
+  return a->in_groups > 0 && a->Cin <= cmax && a->Cin % a->in_groups == 0;
 }
 
 }  // namespace
@@ -1140,7 +1340,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
     const bool gn = p.gmr != nullptr;
-    if (a->Cout % 256 == 0) {
+    if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256))) {
       dim3 g(a->Cout / 256, patches, 1);
       const bool ph2 = hmode != 1 || gn;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
 #define RDMI_HALO(M, P, WN)                                                     \
@@ -1161,13 +1361,27 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
         else
           hipLaunchKernelGGL((conv_halo_kernel<1, 4, 4, false>), g, dim3(512), 0, st, p);
       }
-    } else {
+    } else if (a->Cout == 128 && (hmode == 4 || (gn && a->Cin > 256))) {  // the 8-wave 128-channel variant
       dim3 g(1, patches, 1);
       if (a->upsample)
         RDMI_HALO(2, 1, 2);
       else
         RDMI_HALO(1, 1, 2);
 #undef RDMI_HALO
+    } else {  // two workgroups per CU (RDMI_CONV_HALO=3: also for Cout % 256 == 0)
+      dim3 g((a->Cout + 127) / 128, patches, 1);
+#define RDMI_OCC2(M)                                                                     \
+  do {                                                                                   \
+    if (gn)                                                                              \
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, true>), g, dim3(256), 0, st, p);      \
+    else                                                                                 \
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, false>), g, dim3(256), 0, st, p);     \
+  } while (0)
+      if (a->upsample)
+        RDMI_OCC2(2);
+      else
+        RDMI_OCC2(1);
+#undef RDMI_OCC2
     }
     return rdmi::check_launch("conv2d halo");
   }

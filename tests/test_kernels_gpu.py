@@ -18,13 +18,16 @@ def _k():
     return K
 
 
-@pytest.fixture(params=["auto", "classic", "pingpong", "halo4"])
+@pytest.fixture(params=["auto", "classic", "pingpong", "halo4", "halo128w8"])
 def engine(request, monkeypatch):
-    """GEMM/conv engine: by size (auto: halo conv with 2 phases per K-tile where it applies), the
-    3-slot classic engine only, the ping-pong engine forced for every launch it supports
-    (N % 256 == 0), or the 4-phase halo conv (RDMI_GEMM_PP / RDMI_CONV_HALO, gemm.hip)."""
-    monkeypatch.setenv("RDMI_GEMM_PP", {"auto": "1", "classic": "0", "pingpong": "2", "halo4": "1"}[request.param])
-    monkeypatch.setenv("RDMI_CONV_HALO", {"auto": "2", "classic": "0", "pingpong": "0", "halo4": "1"}[request.param])
+    """GEMM/conv engine: by size (auto: halo conv with 2 phases per K-tile where it applies, the
+    two-workgroups-per-CU halo conv for 128 output channels), the 3-slot classic engine only, the
+    ping-pong engine forced for every launch it supports (N % 256 == 0), the 4-phase halo conv, or
+    the 8-wave 128-channel halo conv (RDMI_GEMM_PP / RDMI_CONV_HALO, gemm.hip)."""
+    pp = {"auto": "1", "classic": "0", "pingpong": "2", "halo4": "1", "halo128w8": "1"}
+    halo = {"auto": "2", "classic": "0", "pingpong": "0", "halo4": "1", "halo128w8": "4"}
+    monkeypatch.setenv("RDMI_GEMM_PP", pp[request.param])
+    monkeypatch.setenv("RDMI_CONV_HALO", halo[request.param])
     return request.param
 
 
@@ -89,7 +92,9 @@ def test_gemm_geglu(engine):
     (1, 15, 17, 64, 512, 1, 1, 0, False),
     # halo engine (3x3 s1 p1, Cin % 64 == 0, 16x16 output patches, Cout % 256 == 0)
     (2, 32, 48, 128, 256, 3, 1, 1, False), (1, 16, 16, 64, 512, 3, 1, 1, False), (1, 8, 16, 192, 256, 3, 1, 1, True),
-    (3, 16, 32, 320, 256, 3, 1, 1, False), (2, 32, 16, 128, 128, 3, 1, 1, False), (1, 16, 8, 256, 128, 3, 1, 1, True)])
+    (3, 16, 32, 320, 256, 3, 1, 1, False), (2, 32, 16, 128, 128, 3, 1, 1, False), (1, 16, 8, 256, 128, 3, 1, 1, True),
+    (1, 16, 32, 128, 384, 3, 1, 1, False), (2, 16, 16, 640, 640, 3, 1, 1, False), (1, 8, 8, 192, 384, 3, 1, 1, True),
+    (2, 16, 32, 320, 320, 3, 1, 1, False), (1, 16, 16, 960, 320, 3, 1, 1, False), (1, 16, 16, 64, 64, 3, 1, 1, False)])
 def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(3)
@@ -188,12 +193,15 @@ def test_groupnorm_moments_from_gemm(engine):
 @pytest.mark.parametrize("B,H,W,Cin,Cout,up,silu,G", [
     (2, 32, 48, 128, 256, False, True, 32), (1, 16, 16, 512, 512, False, True, 32), (2, 8, 16, 256, 256, True, True, 32),
     (2, 32, 16, 128, 128, False, True, 32), (1, 16, 8, 256, 128, True, False, 32), (3, 16, 32, 320, 256, False, True, 32),
-    (1, 16, 16, 1024, 256, False, True, 16), (2, 16, 16, 64, 128, False, True, 8)])
-def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G):
+    (1, 16, 16, 1024, 256, False, True, 16), (2, 16, 16, 64, 128, False, True, 8),
+    (2, 16, 16, 128, 384, False, True, 32), (1, 16, 16, 256, 640, True, True, 32), (2, 16, 16, 192, 320, False, True, 32)])
+def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G, engine):
     """GroupNorm(+SiLU) applied inside the halo conv's input path (rdmi_conv_args.in_*) against the
     unfused groupnorm → conv2d pair on the same data: the same normalised f16 values feed the same
     MFMA order, so the outputs agree bitwise; plus an fp32 torch reference.  Images get distinct
     statistics (per-image scale/offset) so a wrong image index would show."""
+    if engine in ("classic", "pingpong"):
+        pytest.skip("input GroupNorm runs on the halo engines only")
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(21)
     scale = torch.arange(1, B + 1, device=DEV).view(B, 1, 1, 1) * 0.7

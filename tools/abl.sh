@@ -1,9 +1,9 @@
 #!/bin/bash
-# scratch A/B: fused GroupNorm conv, wave priority of the normalising segment
+# scratch A/B: halo conv variants (RDMI_CONV_HALO 2 = default, 3 = two workgroups per CU everywhere)
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for pr in 0 1 2 3; do
-  echo "== RDMI_GN_PRIO=$pr"
-  RDMI_GN_PRIO=$pr timeout -k 10 200 python -u tools/kbench.py --only gnconv || exit 1
+for h in 2 3; do
+  echo "== RDMI_CONV_HALO=$h"
+  RDMI_CONV_HALO=$h timeout -k 10 200 python -u tools/kbench.py --only conv || exit 1
 done
