@@ -1244,12 +1244,11 @@ int halo_mode() {
 }
 
 // 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 output patches,
-// Cout % 64 == 0 (a ragged last 128-channel tile in the two-workgroups-per-CU variant), no
-// per-image row bias.
+// Cout % 64 == 0 (a ragged last 128-channel tile in the two-workgroups-per-CU variant).
 bool halo_eligible(const rdmi_conv_args* a, int hmode) {
   return hmode != 0 && a->kh == 3 && a->kw == 3 && a->Cin % 64 == 0 && a->stride == 1 && a->pad_top == 1 &&
          a->pad_left == 1 && a->Ho % 16 == 0 && a->Wo % 16 == 0 && a->Cout % 64 == 0 &&
-         !a->rowbias && a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
+         a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
 }
 
 // input GroupNorm: groups divide Cin, the LDS scale/shift table holds ≤ 1024 channels (≤ 256 in

@@ -125,6 +125,13 @@ def test_conv2d_vae_downsample_rowbias_residual(engine):
     y2 = K_.conv2d(K_.nchw_to_nhwc(x, C), K_.pack_conv(w.float().cpu(), DEV), C, 3, rowbias=rb, residual=res)
     ref2 = F.conv2d(x.float(), w.float(), padding=1) + rb[:, :, None, None] + res.float().permute(0, 3, 1, 2)
     assert _rel(y2.permute(0, 3, 1, 2), ref2) < 4e-3
+    # per-image time-embedding row bias on the halo engines (UNet conv1: 320 channels, 2 images)
+    x3 = torch.randn(2, 32, 16, 320, device=DEV, generator=g).half()
+    w3 = torch.randn(320, 320, 3, 3, device=DEV, generator=g) / 40
+    rb3 = torch.randn(2, 320, device=DEV, generator=g)
+    y3 = K_.conv2d(x3, K_.pack_conv(w3.cpu(), DEV), 320, 3, rowbias=rb3, gn=True)
+    ref3 = F.conv2d(x3.float().permute(0, 3, 1, 2), w3.half().float(), padding=1) + rb3[:, :, None, None]
+    assert _rel(y3.permute(0, 3, 1, 2), ref3) < 4e-3
 
 
 @pytest.mark.parametrize("C,G,HW,silu,eps", [(320, 32, 9216, True, 1e-5), (128, 32, 1000, False, 1e-6),

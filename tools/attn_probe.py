@@ -1,6 +1,6 @@
 """Run one attention (or conv) shape a few times — a target for rocprofv3 PMC passes.
 
-    python tools/attn_probe.py [--what attn|conv] [--iters 5]"""
+    python tools/attn_probe.py [--what attn|conv] [--iters 5] [--shape B,H,W,Cin,Cout]"""
 import argparse
 import math
 import os
@@ -14,6 +14,7 @@ from rollingdepth_amd import kernels as K  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--what", default="attn")
 ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--shape", default="8,192,192,512,512", help="conv: B,H,W,Cin,Cout")
 a = ap.parse_args()
 torch.manual_seed(0)
 if a.what == "attn":
@@ -24,7 +25,7 @@ if a.what == "attn":
     out = torch.empty(B, S, C, device="cuda", dtype=torch.float16)
     fn = lambda: K.attention(q, k, v, H, out=out)  # noqa: E731
 else:
-    B, H, W, ci, co = 8, 192, 192, 512, 512
+    B, H, W, ci, co = (int(v) for v in a.shape.split(","))
     x = torch.randn(B, H, W, ci, device="cuda").half()
     w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
     out = torch.empty(B, H, W, co, device="cuda", dtype=torch.float16)
