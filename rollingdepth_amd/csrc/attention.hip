@@ -380,6 +380,57 @@ __global__ __launch_bounds__(256) void softmax_rows_k(const float* __restrict__ 
   for (long c = cols + threadIdx.x; c < p_ld; c += 256) pr[c] = (f16)0.f;  // K padding of the PV GEMM
 }
 
+// Single-pass row softmax: the row (≤ 1024·NV floats) is read once into registers as float4s,
+// max and sum are block reductions, and the probabilities are written from registers — one HBM
+// read of the f32 scores instead of three (the scores of a 96² VAE attention are 36 KiB rows
+// that the L2 does not hold across three passes with every CU streaming).
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_rows_reg_k(const float* __restrict__ s, f16* __restrict__ pout, long cols,
+                                                          long p_ld, float scale) {
+  const long row = blockIdx.x;
+  const f32x4* sr = (const f32x4*)(s + row * cols);
+  const int nv = (int)(cols >> 2);
+  __shared__ float red[4];
+  f32x4 v[NV];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    v[i] = c < nv ? sr[c] : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    mx = fmaxf(mx, fmaxf(fmaxf(v[i][0], v[i][1]), fmaxf(v[i][2], v[i][3])));
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[i][e] = __expf((v[i][e] - mx) * scale);
+      sum += v[i][e];
+    }
+  sum = wave_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  sum = red[0] + red[1] + red[2] + red[3];
+  const float inv = 1.f / sum;
+  f16* pr = pout + row * p_ld;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = threadIdx.x + 256 * i;
+    if (c < nv) {
+      f16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (f16)(v[i][e] * inv);
+      *(f16x4*)(pr + 4 * c) = o;
+    }
+  }
+  for (long c = cols + threadIdx.x; c < p_ld; c += 256) pr[c] = (f16)0.f;  // K padding of the PV GEMM
+}
+
 }  // namespace
 
 extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
@@ -412,7 +463,14 @@ extern "C" int rdmi_attention_smallkv(const void* q, const void* k, const void* 
 
 extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, void* stream) {
   RDMI_REQUIRE(s && p && rows > 0 && cols > 0 && p_ld >= cols, RDMI_E_ARG, "softmax_rows: bad args");
-  hipLaunchKernelGGL(softmax_rows_k, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, s, (f16*)p, cols, p_ld,
-                     scale);
+  hipStream_t st = (hipStream_t)stream;
+  const bool vec = cols % 4 == 0 && p_ld % 4 == 0 && ((uintptr_t)s & 15) == 0 && ((uintptr_t)p & 7) == 0;
+  const long nv = (cols / 4 + 255) / 256;  // float4s per thread
+  if (vec && nv <= 4)
+    hipLaunchKernelGGL(softmax_rows_reg_k<4>, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
+  else if (vec && nv <= 16)
+    hipLaunchKernelGGL(softmax_rows_reg_k<16>, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
+  else
+    hipLaunchKernelGGL(softmax_rows_k, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
   return rdmi::check_launch("softmax_rows");
 }

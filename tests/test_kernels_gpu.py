@@ -363,6 +363,20 @@ def test_attention_smallkv():
     assert (o.float() - ref).abs().max().item() < 3e-3
 
 
+@pytest.mark.parametrize("cols,pad", [(9216, 0), (5000, 8), (20000, 0), (1024, 0), (234, 6), (36, 4)])
+def test_softmax_rows(cols, pad):
+    """Row softmax (single-pass register kernel for cols % 4 == 0 and ≤ 16384, three-pass
+    otherwise) against torch.softmax; the padding columns are written as zeros."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    s = torch.randn(37, cols, device=DEV, generator=g) * 8
+    out = torch.full((37, cols + pad), 7.0, device=DEV, dtype=torch.float16)
+    p = K_.softmax_rows(s, 0.3, out=out)
+    ref = torch.softmax(s * 0.3, dim=-1)
+    assert (p[:, :cols].float() - ref).abs().max().item() < 2e-3
+    assert torch.all(p[:, cols:] == 0)
+
+
 @pytest.mark.parametrize("S", [256, 234, 97])
 def test_vae_style_attention_via_gemm(S):
     """GEMM(f32 scores) → softmax_rows → GEMM with Vᵀ, the d=C single-head path (attention_1head);
