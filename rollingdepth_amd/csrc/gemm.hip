@@ -1139,6 +1139,115 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq);
 }
 
+// Two-workgroups-per-CU dense GEMM (the UNet's single-batch Linears).  A 256×256
+// ping-pong tile over K = 320 runs only 5 K-tiles between a DMA prologue and a 128-KiB epilogue
+// that one workgroup per CU cannot overlap, and such GEMMs move as many bytes (A in, C out) as
+// they compute: their bound is the stream, not the MFMAs.  Here 4-wave workgroups own 128×128
+// tiles (64×64 per wave) in a 64-KiB 2-slot LDS ring, two per CU, so one workgroup's epilogue
+// stores and next prologue run under the other's K loop.  Per K-tile as conv_halo_occ2_kernel:
+// wait for the own DMA of this K-tile (issued one K-tile earlier) and the own fragment reads of
+// the previous one, one barrier, issue the next K-tile into the other slot, 16 fragment reads,
+// 32 MFMAs.  LDS rows are 128 B with 16-B chunk c of row r at c ^ (r & 7) (as gemm_pp_kernel).
+__global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
+  constexpr int BM = 128, BN = 128, BKP = 64, RM = 4, RN = 4;
+  constexpr int NA = 4, NB = 4;            // 1-KiB DMA pieces per wave per K-tile (16 / 4 waves each)
+  constexpr int SLOT = (BM + BN) * BKP;    // halves (32 KiB)
+  __shared__ __attribute__((aligned(16))) f16 lds[2 * SLOT];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nbx = gridDim.x;
+  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+  int mt_, nt_;
+  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN, m0 = mt_ * BM;
+  const int bz = blockIdx.z;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)bz * p.sA), (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.Wt + (long)bz * p.sW), (short)0, (int)p.w_bytes, 0x00020000);
+
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ lrow;
+  int arow[NA], brow[NB];
+#pragma unroll
+  for (int e = 0; e < NA; ++e) {
+    const int m = m0 + (wid + 4 * e) * 8 + lrow;
+    arow[e] = m < p.M ? m * (int)p.lda : -1;
+  }
+#pragma unroll
+  for (int e = 0; e < NB; ++e) {
+    const int n = n0 + (wid + 4 * e) * 8 + lrow;
+    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+  }
+  auto issue = [&](int u) {
+    const int kk = u * BKP + chunk * 8;
+    const bool kok = kk < p.Kvalid;
+    f16* la = lds + (u & 1) * SLOT;
+    f16* lb = la + BM * BKP;
+#pragma unroll
+    for (int e = 0; e < NA; ++e)
+      dma16(ra_, arow[e] >= 0 && kok ? (unsigned)(arow[e] + kk) * 2u : OOB, la + (wid + 4 * e) * 8 * BKP);
+#pragma unroll
+    for (int e = 0; e < NB; ++e)
+      dma16(rw_, brow[e] >= 0 && kok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 4 * e) * 8 * BKP);
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BKP - 1) / BKP;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
+  const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
+
+  issue(0);
+  wait_vmcnt<0>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int u = 0; u < nk; ++u) {
+    if (u > 0) {
+      wait_vmcnt<0>();  // this K-tile, issued one K-tile ago
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot issue() refills
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (u + 1 < nk) issue(u + 1);
+    const f16* la = lds + (u & 1) * SLOT + (wm * 64) * BKP;
+    const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * 64) * BKP;
+    f16x8 af[2][RM], bf[2][RN];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int off = kh ? off1 : off0;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+#pragma unroll
+      for (int i = 0; i < RM; ++i) af[kh][i] = *(const f16x8*)(la + i * 16 * BKP + off);
+    }
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
+  }
+  store_tile<RM, RN, 64>(p, acc, LinRows{m0 + wm * 64, fr, p.M}, n0 + wn * 64, bz, fr, fq);
+}
+
+// Two-workgroups-per-CU GEMM engine (RDMI_GEMM_OCC2, read per launch for A/B: 0 off, 2 every
+// dense GEMM, unset/1 = the measured policy in launch_mode)
+int occ2_mode() {
+  const char* e = getenv("RDMI_GEMM_OCC2");
+  return e ? atoi(e) : 1;
+}
+
 // Engine choice.  RDMI_GEMM_PP (read per launch; for tests and A/B measurements): 0 = classic
 // engine only, 2 = a ping-pong tile whenever the shape allows one, unset/1 = by estimated cost.
 int pp_mode() {
@@ -1162,6 +1271,19 @@ void launch_pp(const GemmP& p, int batch, hipStream_t s) {
 
 template <int MODE>
 void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
+  if (MODE == 0) {
+    // measured policy (tools/kbench.py gemm, profiles/r01_gemm_occ2_ab.log): the two-workgroups-
+    // per-CU engine wins on the UNet's single-batch Linears without a 256×256 ping-pong tile
+    // (N % 256 != 0: +4…18 %) or with a long K (N = 1280, K = 5120: +19 %), and loses on the
+    // GEGLU projections, the batched VAE attention GEMMs and N % 256 == 0 with short K (−9…18 %)
+    const int oc = occ2_mode();
+    const bool pick = !p.geglu && batch == 1 && !p.c_f32 && p.N <= 1920 && (p.N % 256 != 0 || p.K >= 2048);
+    if (oc == 2 || (oc == 1 && pick)) {
+      dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
+      hipLaunchKernelGGL(gemm_occ2_kernel, g, dim3(256), 0, s, p);
+      return;
+    }
+  }
   const int pp = pp_mode();
   // ping-pong candidates (N must be a multiple of the tile width; conv needs 64-channel blocks)
   if (pp != 0 && (MODE == 0 || p.cmaj)) {

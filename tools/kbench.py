@@ -99,12 +99,29 @@ def bench_cinsweep(iters):
 def bench_gemm(iters):
     for lab, M, N, Kd, geglu in [("L0 qkv 221k x 960 x 320", 221184, 960, 320, False),
                                  ("L0 ff1 geglu 221k x 2560 x 320", 221184, 2560, 320, True),
+                                 ("L0 proj 221k x 320 x 320 +res", 221184, 320, 320, False),
+                                 ("L1 proj 55k x 640 x 640 +res", 55296, 640, 640, False),
+                                 ("L1 ff1 geglu 55k x 5120 x 640", 55296, 5120, 640, True),
                                  ("L0 ff2 221k x 320 x 1280", 221184, 320, 1280, False),
                                  ("L2 ff1 geglu 13.8k x 10240 x 1280", 13824, 10240, 1280, True),
-                                 ("L2 ff2 13.8k x 1280 x 5120", 13824, 1280, 5120, False)]:
+                                 ("L2 ff2 13.8k x 1280 x 5120", 13824, 1280, 5120, False),
+                                 ("L1 qkv 55k x 1920 x 640", 55296, 1920, 640, False),
+                                 ("L2 qkv 13.8k x 3840 x 1280", 13824, 3840, 1280, False),
+                                 ("vae qkv 73.7k x 1536 x 512", 73728, 1536, 512, False),
+                                 ("vae scores b8 9216 x 9216 x 512 f32", 9216, 9216, 512, False),
+                                 ("vae pv b8 9216 x 512 x 9216", 9216, 512, 9216, False)]:
+        if " b8 " in lab:  # batched, operands as the VAE attention has them
+            a = torch.randn(8, M, Kd, device="cuda").half()
+            w = torch.randn(8, N, Kd, device="cuda").half()
+            f32 = "f32" in lab
+            ms = timeit(lambda: K.gemm(a, w, Kd, out_f32=f32), iters)
+            fl = 2.0 * 8 * M * N * Kd
+            print(f"gemm  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
+            continue
         a = torch.randn(M, Kd, device="cuda").half()
         w = K.pack_linear(torch.randn(N, Kd) / math.sqrt(Kd), "cuda")
-        ms = timeit(lambda: K.gemm(a, w, Kd, geglu=geglu), iters)
+        r = torch.randn(M, N, device="cuda").half() if "+res" in lab else None
+        ms = timeit(lambda: K.gemm(a, w, Kd, geglu=geglu, residual=r), iters)
         fl = 2.0 * M * N * Kd
         print(f"gemm  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
