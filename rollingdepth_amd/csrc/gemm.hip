@@ -54,6 +54,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f
 // dimension, or the rows of a 16-pixel-wide spatial patch (conv_halo_kernel).  slot(i): the
 // 32-row GroupNorm-moment slot of the fragment pair (i-1, i) (rdmi.h gn_part); every image's slots
 // are the contiguous range [b·HW/32, (b+1)·HW/32) in both maps.
+// full(n): every row of the wave's n fragments exists; group(n, rpg): the one row-bias group
+// (rows / rpg) all those rows fall in, or -1 when they straddle groups (wave-uniform).
 struct LinRows {
   int mw, fr, M;
   __device__ int row(int i) const {
@@ -61,11 +63,15 @@ struct LinRows {
     return m < M ? m : -1;
   }
   __device__ long slot(int i) const { return (mw + (i - 1) * 16) >> 5; }
+  __device__ bool full(int n) const { return mw + n * 16 <= M; }
+  __device__ int group(int n, int rpg) const { return mw / rpg == (mw + n * 16 - 1) / rpg ? mw / rpg : -1; }
 };
 struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; Ho even, Wo % 16 == 0
   int b, Ho, Wo, y0, x0, rw, fr;
   __device__ int row(int i) const { return (b * Ho + y0 + rw + i) * Wo + x0 + fr; }
   __device__ long slot(int i) const { return (long)((b * Ho + y0 + rw + i - 1) >> 1) * (Wo >> 4) + (x0 >> 4); }
+  __device__ bool full(int) const { return true; }
+  __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }  // conv: rpg = Ho·Wo
 };
 
 template <int RM, int RN, int WTN, class Rows>
@@ -73,6 +79,69 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
                                            int fr, int fq) {
   const long cb = (long)bz * p.sC;
   const long rbz = (long)bz * p.sR;
+  // Fast path for whole f16 tiles (every row exists, every 4-column group inside N, one row-bias
+  // group): all operand loads (bias, row bias, residual) are issued before the first use, so the
+  // wave waits for memory once instead of once per fragment.
+  const int rbg = p.rowbias ? rows.group(RM, p.rpg) : 0;
+  if (!p.geglu && !p.c_f32 && p.vec && rows.full(RM) && nw + RN * 16 <= p.N && rbg >= 0) {
+    f32x4 badd[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int n = nw + j * 16 + fq * 4;
+      badd[j] = p.bias ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (p.rowbias) badd[j] += *(const f32x4*)(p.rowbias + (long)rbg * p.rb_ld + n);
+    }
+    f16x4 rr[RM][RN];
+    if (p.R) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          rr[i][j] = *(const f16x4*)(p.R + rbz + (long)rows.row(i) * p.ldr + nw + j * 16 + fq * 4);
+    }
+    float gs[RN], gq[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const long crow = cb + (long)rows.row(i) * p.ldc;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = nw + j * 16 + fq * 4;
+        f16x4 o;
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] * p.alpha + badd[j][r];
+          if (p.R) v += (float)rr[i][j][r];
+          if (p.silu) v = silu_f(v);
+          o[r] = (f16)v;
+          const float f = (float)o[r];
+          s += f;
+          q = fmaf(f, f, q);
+        }
+        *(f16x4*)((f16*)p.C + crow + n) = o;
+        if (p.gnp) {  // as below: fixed butterfly over the 16 rows of the fragment pair
+          if (!(i & 1)) {
+            gs[j] = s;
+            gq[j] = q;
+          } else {
+            s += gs[j];
+            q += gq[j];
+#pragma unroll
+            for (int o2 = 1; o2 < 16; o2 <<= 1) {
+              s += __shfl_xor(s, o2, 64);
+              q += __shfl_xor(q, o2, 64);
+            }
+            if (fr == 0) {
+              float* d = p.gnp + (long)(n >> 2) * p.gn_ld + rows.slot(i) * 2;
+              d[0] = s;
+              d[1] = q;
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
   if (!p.geglu) {
     static_assert(RM % 2 == 0, "GroupNorm moments pair 16-row tiles into 32-row blocks");
     float gs[RN], gq[RN];  // per column tile: moments of this lane's 4 outputs over a 32-row block
