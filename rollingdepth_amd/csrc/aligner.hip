@@ -21,6 +21,10 @@
 namespace {
 
 constexpr int MAXD = 8;
+// Pixel chunks per frame / per snippet: frame_stats and snippet_grad run N·PS and ntot·PS
+// workgroups (one workgroup per frame or snippet alone left most of the 256 CUs idle and each
+// latency-bound), partial sums combined in a fixed chunk order by the consumer (deterministic).
+constexpr int PS = 8;
 
 struct AlP {
   const float* x[MAXD];
@@ -31,8 +35,9 @@ struct AlP {
   long P;
   float lr, b1, b2, eps, lmda2, lmda3, dw, ls;
   // workspace views
-  float *T, *Td, *scale, *scaled, *fmin, *fmax;
-  double *gs, *gt, *l1, *l2;
+  float *T, *Td;
+  double* fpart;  // [N][PS][4]: Σ|T|, Σ|Td|, min T, max T over pixel chunk c of frame f
+  double *gs, *gt, *l1, *l2;  // [ntot][PS]: per snippet and pixel chunk
   float *m, *v;  // Adam moments [2*Ntot] (s then t)
   float* hist;
   int ntot;
@@ -54,12 +59,15 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
   return r;
 }
 
+__device__ __forceinline__ long chunk_lo(long P, int c) { return P * c / PS; }
+
 __global__ __launch_bounds__(256) void frame_stats(AlP p) {
-  const int f = blockIdx.x;
+  const int f = blockIdx.x, c = blockIdx.y;
   __shared__ double sh[8];
   double sa = 0.0, sd = 0.0;
   float mn = INFINITY, mx = -INFINITY;
-  for (long px = threadIdx.x; px < p.P; px += 256) {
+  const long p1 = chunk_lo(p.P, c + 1);
+  for (long px = chunk_lo(p.P, c) + threadIdx.x; px < p1; px += 256) {
     float sum = 0.f, sumd = 0.f;
     int cnt = 0;
     for (int d = 0; d < p.nd; ++d) {
@@ -96,15 +104,29 @@ __global__ __launch_bounds__(256) void frame_stats(AlP p) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    p.scale[f] = (float)(A / (double)p.P);
-    p.scaled[f] = (float)(D / (double)p.P);
-    p.fmin[f] = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
-    p.fmax[f] = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
+    double* o = p.fpart + ((long)f * PS + c) * 4;
+    o[0] = A;
+    o[1] = D;
+    o[2] = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
+    o[3] = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
   }
+}
+
+// per-frame L1 scales mean|T|, mean|Td| (:197-198) from the chunk partials, chunk order fixed
+__device__ __forceinline__ void frame_scales(const AlP& p, int f, float& sc, float& scd) {
+  double A = 0.0, D = 0.0;
+  for (int c = 0; c < PS; ++c) {
+    A += p.fpart[((long)f * PS + c) * 4];
+    D += p.fpart[((long)f * PS + c) * 4 + 1];
+  }
+  sc = (float)(A / (double)p.P);
+  scd = (float)(D / (double)p.P);
 }
 
 __global__ __launch_bounds__(256) void snippet_grad(AlP p) {
   const int gk = blockIdx.x;  // global snippet index
+  const int c = blockIdx.y;   // pixel chunk
+  const long p0 = chunk_lo(p.P, c), p1 = chunk_lo(p.P, c + 1);
   int d = 0;
   while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
   const int k = gk - p.off[d];
@@ -113,10 +135,12 @@ __global__ __launch_bounds__(256) void snippet_grad(AlP p) {
   double gs = 0.0, gt = 0.0, l1 = 0.0, l2 = 0.0;
   for (int j = 0; j < p.w; ++j) {
     const int f = k + j * p.stride[d];
-    const float isc = 1.0f / p.scale[f], iscd = 1.0f / p.scaled[f];
+    float scf, scdf;
+    frame_scales(p, f, scf, scdf);
+    const float isc = 1.0f / scf, iscd = 1.0f / scdf;
     const float* Tf = p.T + (long)f * p.P;
     const float* Tdf = p.Td + (long)f * p.P;
-    for (long px = threadIdx.x; px < p.P; px += 256) {
+    for (long px = p0 + threadIdx.x; px < p1; px += 256) {
       float xv = x[(long)j * p.P + px];
       float a = addrn(mulrn(xv, s), t);
       float z = a - Tf[px];
@@ -139,10 +163,11 @@ __global__ __launch_bounds__(256) void snippet_grad(AlP p) {
   l1 = block_sum_d<256>(l1, sh);
   l2 = block_sum_d<256>(l2, sh);
   if (threadIdx.x == 0) {
-    p.gs[gk] = gs;
-    p.gt[gk] = gt;
-    p.l1[gk] = l1;
-    p.l2[gk] = l2;
+    const long o = (long)gk * PS + c;
+    p.gs[o] = gs;
+    p.gt[o] = gt;
+    p.l1[o] = l1;
+    p.l2[o] = l2;
   }
 }
 
@@ -150,7 +175,7 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
   __shared__ double sh[8];
   // loss history (uses the parameters BEFORE this update, like the closure's loss)
   double L1 = 0.0, L2 = 0.0, soft = 0.0;
-  for (int i = threadIdx.x; i < p.ntot; i += 256) {
+  for (int i = threadIdx.x; i < p.ntot * PS; i += 256) {
     L1 += p.l1[i];
     L2 += p.l2[i];
   }
@@ -167,12 +192,22 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
     b = block_sum_d<256>(b, sh);
     soft += p.lmda2 * a / p.n[d] + p.lmda3 * b / p.n[d];
   }
+  float mn = INFINITY, mx = -INFINITY;
+  for (long i = threadIdx.x; i < (long)p.N * PS; i += 256) {
+    mn = fminf(mn, (float)p.fpart[i * 4 + 2]);
+    mx = fmaxf(mx, (float)p.fpart[i * 4 + 3]);
+  }
+  mn = wave_min(mn);
+  mx = wave_max(mx);
+  __shared__ float rmm[2][4];
+  if ((threadIdx.x & 63) == 0) {
+    rmm[0][threadIdx.x >> 6] = mn;
+    rmm[1][threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
   if (p.hist && threadIdx.x == 0) {
-    float mn = INFINITY, mx = -INFINITY;
-    for (int f = 0; f < p.N; ++f) {
-      mn = fminf(mn, p.fmin[f]);
-      mx = fmaxf(mx, p.fmax[f]);
-    }
+    mn = fminf(fminf(rmm[0][0], rmm[0][1]), fminf(rmm[0][2], rmm[0][3]));
+    mx = fmaxf(fmaxf(rmm[1][0], rmm[1][1]), fmaxf(rmm[1][2], rmm[1][3]));
     float* h = p.hist + 3L * (step - 1);
     h[0] = (float)(p.ls * (L1 / denom + p.dw * L2 / denom) + soft);
     h[1] = mn;
@@ -194,7 +229,10 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
     const int k = gk - p.off[d];
     float* prm = is_t ? &p.t[d][k] : &p.s[d][k];
     const float pv = *prm;
-    float g = (float)((is_t ? p.gt[gk] : p.gs[gk]) * (double)gscale);
+    const double* gp = (is_t ? p.gt : p.gs) + (long)gk * PS;
+    double gsum = 0.0;
+    for (int c = 0; c < PS; ++c) gsum += gp[c];
+    float g = (float)(gsum * (double)gscale);
     const float nd = (float)p.n[d];
     if (!is_t) {
       float r = fmaxf(0.f, 1.f - pv);
@@ -283,8 +321,8 @@ __global__ void prepare_k(PrepP p) {
 }
 
 long ws_floats(int N, long P, int ntot) {
-  // T, Td (N*P each), scale, scaled, fmin, fmax (N each), 4 double arrays (ntot each), m, v (2*ntot each)
-  return 2L * N * P + 4L * N + 8L * ntot + 4L * ntot + 64;
+  // 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v (2·ntot each)
+  return 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + 64;
 }
 
 }  // namespace
@@ -321,14 +359,12 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   float* w = a->workspace;
   RDMI_REQUIRE(((uintptr_t)w & 7) == 0, RDMI_E_ALIGN, "aligner: workspace must be 8-byte aligned");
   double* dw = (double*)w;
-  p.gs = dw; p.gt = dw + ntot; p.l1 = dw + 2 * ntot; p.l2 = dw + 3 * ntot;
-  float* fw = (float*)(dw + 4 * ntot);
+  const long nps = (long)ntot * PS;
+  p.gs = dw; p.gt = dw + nps; p.l1 = dw + 2 * nps; p.l2 = dw + 3 * nps;
+  p.fpart = dw + 4 * nps;
+  float* fw = (float*)(p.fpart + 4L * p.N * PS);
   p.T = fw; fw += (long)p.N * p.P;
   p.Td = fw; fw += (long)p.N * p.P;
-  p.scale = fw; fw += p.N;
-  p.scaled = fw; fw += p.N;
-  p.fmin = fw; fw += p.N;
-  p.fmax = fw; fw += p.N;
   p.m = fw; fw += 2 * ntot;
   p.v = fw; fw += 2 * ntot;
   p.hist = a->history;
@@ -339,8 +375,8 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   int rc = rdmi::check_launch("aligner_zero");
   if (rc) return rc;
   for (int it = 1; it <= a->iters; ++it) {
-    hipLaunchKernelGGL(frame_stats, dim3(p.N), dim3(256), 0, st, p);
-    hipLaunchKernelGGL(snippet_grad, dim3(ntot), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(frame_stats, dim3(p.N, PS), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(snippet_grad, dim3(ntot, PS), dim3(256), 0, st, p);
     hipLaunchKernelGGL(adam_step, dim3(1), dim3(256), 0, st, p, it, denom);
     rc = rdmi::check_launch("aligner_iteration");
     if (rc) return rc;
