@@ -1,9 +1,9 @@
 #!/bin/bash
-# scratch A/B: halo conv variants with the fused input GroupNorm (RDMI_CONV_HALO 2 = default, 3 = two workgroups per CU everywhere)
+# scratch A/B: attention wave priority (RDMI_ATTN_PRIO 0 = flips around MFMA blocks, 1 = none, 2 = static for waves 4-7)
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for h in 2 3; do
-  echo "== RDMI_CONV_HALO=$h"
-  RDMI_CONV_HALO=$h timeout -k 10 200 python -u tools/kbench.py --only gnconv || exit 1
+for pr in 0 1 2 0; do
+  echo "== RDMI_ATTN_PRIO=$pr"
+  RDMI_ATTN_PRIO=$pr timeout -k 10 200 python -u tools/kbench.py --only attn || exit 1
 done
