@@ -60,6 +60,79 @@ __global__ __launch_bounds__(HT) void head_taps(const f16* __restrict__ x, long 
   for (int t = 0; t < 9; ++t) d[t * P + q] = acc[t];
 }
 
+// pass 1, coalesced form (C = 8·LPP, LPP a power of two ≤ 64): LPP lanes share a pixel, each
+// normalising and weighting 8 channels, so one wave load instruction reads 64/LPP whole pixel
+// rows (the per-thread form above reads 64 rows 2·C bytes apart per instruction); the 9 tap sums
+// are reduced across the LPP lanes in a fixed butterfly and written pixel-major, d[p][9].
+template <int LPP>
+__global__ __launch_bounds__(HT) void head_taps_v(const f16* __restrict__ x, long HW, int G,
+                                                  const float* __restrict__ mr, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, const float* __restrict__ w,
+                                                  int silu, float* __restrict__ d, long P, int ppb) {
+  constexpr int C = 8 * LPP;
+  const int b = blockIdx.y;
+  const int cl = threadIdx.x % LPP;  // channel chunk of this lane
+  const int c0 = cl * 8;
+  const int cpg = C / G;
+  float sc[8], sh[8], wt[9][8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    const float mean = mr[2 * (b * G + g)], rstd = mr[2 * (b * G + g) + 1];
+    sc[e] = rstd * gamma[c];
+    sh[e] = beta[c] - mean * sc[e];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) wt[t][e] = w[t * C + c];
+  }
+  const long pbeg = (long)blockIdx.x * ppb;
+  const long pend = pbeg + ppb < HW ? pbeg + ppb : HW;
+  for (long p = pbeg + threadIdx.x / LPP; p < pend; p += HT / LPP) {
+    const f16x8 v = *(const f16x8*)(x + ((long)b * HW + p) * C + c0);
+    float acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float f = fmaf((float)v[e], sc[e], sh[e]);
+      if (silu) f = silu_f(f);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[t] = fmaf(f, wt[t][e], acc[t]);
+    }
+#pragma unroll
+    for (int o = 1; o < LPP; o <<= 1)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[t] += __shfl_xor(acc[t], o, 64);
+    float* dp = d + ((long)b * HW + p) * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      if (t % LPP == cl) dp[t] = acc[t];  // tap t written by lane t mod LPP of the group
+  }
+}
+
+// pass 2 for the pixel-major taps: out[q] = bias + Σ_{dy,dx} d[q + (dy-1)·W + dx-1][3dy+dx]
+__global__ __launch_bounds__(HT) void head_gather_v(const float* __restrict__ d, int H, int W, long P, float bias,
+                                                    f16* __restrict__ out) {
+  const long q = (long)blockIdx.x * HT + threadIdx.x;
+  if (q >= P) return;
+  const long HW = (long)H * W;
+  const long b = q / HW;
+  const int r = (int)(q - b * HW);
+  const int h = r / W, wc = r - (r / W) * W;
+  float s = bias;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int hh = h + dy - 1;
+    if ((unsigned)hh >= (unsigned)H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int ww = wc + dx - 1;
+      if ((unsigned)ww >= (unsigned)W) continue;
+      s += d[(b * HW + (long)hh * W + ww) * 9 + 3 * dy + dx];
+    }
+  }
+  out[q] = (f16)s;
+}
+
 // pass 2: out[b][h][w] = bias + Σ_{dy,dx} d[3dy+dx][b][h+dy-1][w+dx-1] (zero outside the image)
 __global__ __launch_bounds__(HT) void head_gather(const float* __restrict__ d, int H, int W, long P, float bias,
                                                   f16* __restrict__ out) {
@@ -97,6 +170,25 @@ extern "C" int rdmi_conv3x3_to1_gn(const void* x, int B, int H, int W, int C, in
   RDMI_REQUIRE(((uintptr_t)x & 15) == 0, RDMI_E_ALIGN, "conv3x3_to1_gn: x not 16-byte aligned");
   const long HW = (long)H * W, P = (long)B * HW;
   hipStream_t s = (hipStream_t)stream;
+  const int lpp = C / 8;
+  if (lpp == 16 || lpp == 32 || lpp == 64 || lpp == 8 || lpp == 4 || lpp == 2 || lpp == 1) {
+    constexpr int PPB = 1024;  // pixels per workgroup
+    dim3 g(rdmi::div_up(HW, PPB), B);
+#define RDMI_HEAD(L)                                                                                        \
+  case L:                                                                                                   \
+    hipLaunchKernelGGL(head_taps_v<L>, g, dim3(HT), 0, s, (const f16*)x, HW, G, mean_rstd, gamma, beta, w, \
+                       silu, workspace, P, PPB);                                                            \
+    break;
+    switch (lpp) {
+      RDMI_HEAD(1) RDMI_HEAD(2) RDMI_HEAD(4) RDMI_HEAD(8) RDMI_HEAD(16) RDMI_HEAD(32) RDMI_HEAD(64)
+      default: break;
+    }
+#undef RDMI_HEAD
+    int rc = rdmi::check_launch("conv3x3_to1_gn taps");
+    if (rc) return rc;
+    hipLaunchKernelGGL(head_gather_v, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (f16*)y);
+    return rdmi::check_launch("conv3x3_to1_gn gather");
+  }
   const size_t lds = (size_t)11 * C * sizeof(float);
   hipLaunchKernelGGL(head_taps, dim3(rdmi::div_up(HW, HT), B), dim3(HT), lds, s, (const f16*)x, HW, C, G, mean_rstd,
                      gamma, beta, w, silu, workspace, P);

@@ -55,6 +55,17 @@ def bench_conv(iters):
         print(f"conv  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
 
+def bench_head(iters):
+    """Decoder head: GroupNorm+SiLU+3x3 conv to one channel (rdmi_conv3x3_to1_gn)."""
+    for B, H, C in [(16, 768, 128), (8, 768, 128)]:
+        x = torch.randn(B, H, H, C, device="cuda").half()
+        g, b = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+        w9 = torch.randn(9, C, device="cuda") / 30
+        out = torch.empty(B, H, H, 1, device="cuda", dtype=torch.float16)
+        ms = timeit(lambda: K.conv3x3_to1_gn(x, g, b, 32, 1e-6, True, w9, 0.1, out=out), iters)
+        print(f"head  B={B} {H}^2 C={C}                {ms * 1e3:9.1f} us  {x.numel() * 2 / ms / 1e6:8.0f} GB/s (input)")
+
+
 def bench_gnconv(iters):
     """GroupNorm+SiLU → conv: apply pass + conv vs the norm fused into the halo conv's input."""
     from rollingdepth_amd._native import lib
@@ -206,4 +217,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
