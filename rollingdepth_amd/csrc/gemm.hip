@@ -54,6 +54,23 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f
 // dimension, or the rows of a 16-pixel-wide spatial patch (conv_halo_kernel).  slot(i): the
 // 32-row GroupNorm-moment slot of the fragment pair (i-1, i) (rdmi.h gn_part); every image's slots
 // are the contiguous range [b·HW/32, (b+1)·HW/32) in both maps.
+// Sum over the 16 lanes of a DPP row (the 16 rows of an MFMA fragment) with VALU DPP adds — the
+// xor-1, xor-2 butterfly (quad_perm) then the 4- and 8-lane halves (row_half_mirror, row_mirror:
+// every lane of a quad / half-row holds the same partial, so the mirror pairs add the same two
+// operands as xor-4 / xor-8 would).  Replaces ds_bpermute shuffles (LDS round trips) in the
+// GroupNorm-moment epilogue; the sum order is unchanged.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8-lane half
+  v += dpp_f<0x140>(v);  // row_mirror: the other half of the row
+  return v;
+}
+
 // full(n): every row of the wave's n fragments exists; group(n, rpg): the one row-bias group
 // (rows / rpg) all those rows fall in, or -1 when they straddle groups (wave-uniform).
 struct LinRows {
@@ -126,11 +143,8 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
           } else {
             s += gs[j];
             q += gq[j];
-#pragma unroll
-            for (int o2 = 1; o2 < 16; o2 <<= 1) {
-              s += __shfl_xor(s, o2, 64);
-              q += __shfl_xor(q, o2, 64);
-            }
+            s = row16_sum(s);
+            q = row16_sum(q);
             if (fr == 0) {
               float* d = p.gnp + (long)(n >> 2) * p.gn_ld + rows.slot(i) * 2;
               d[0] = s;
@@ -219,11 +233,8 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
           } else {
             s += gs[j];
             q += gq[j];
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) {  // fixed butterfly over the 16 rows of the tile
-              s += __shfl_xor(s, o, 64);
-              q += __shfl_xor(q, o, 64);
-            }
+            s = row16_sum(s);  // fixed butterfly over the 16 rows of the tile
+            q = row16_sum(q);
             if (fr == 0 && ok) {
               float* d = p.gnp + (long)(n >> 2) * p.gn_ld + rows.slot(i) * 2;
               d[0] = s;

@@ -88,8 +88,16 @@ def bench_gnconv(iters):
         ms_u = timeit(unfused, iters)
         ms_f = timeit(lambda: K.conv2d(x, w, co, 3, upsample=up, out=out, in_gn=(mr, g, b, 32, True)), iters)
         fl = 2.0 * B * Ho * Wo * co * ci * 9
+        res = torch.randn(B, Ho, Wo, co, device="cuda").half()
+        # as ResnetBlock2D.conv2 runs it: + residual, GroupNorm moments of the output for the next norm
+        ms_r = timeit(lambda: K.conv2d(x, w, co, 3, upsample=up, out=out, in_gn=(mr, g, b, 32, True), residual=res,
+                                       gn=True), iters)
+        ms_r1 = timeit(lambda: K.conv2d(x, w, co, 3, upsample=up, out=out, in_gn=(mr, g, b, 32, True), residual=res),
+                       iters)
+        ms_m1 = timeit(lambda: K.conv2d(x, w, co, 3, upsample=up, out=out, in_gn=(mr, g, b, 32, True), gn=True), iters)
         print(f"gnconv {lab:31s} apply+conv {ms_u * 1e3:9.1f} us | fused {ms_f * 1e3:9.1f} us "
-              f"{fl / ms_f / 1e9:8.1f} TFLOP/s")
+              f"{fl / ms_f / 1e9:8.1f} TFLOP/s | +res+moments {ms_r * 1e3:9.1f} us {fl / ms_r / 1e9:8.1f} TFLOP/s"
+              f" | +res {ms_r1 * 1e3:9.1f} | +moments {ms_m1 * 1e3:9.1f}")
 
 
 def bench_cinsweep(iters):
