@@ -247,7 +247,16 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
   } else if constexpr (WTN == 64) {
     // GEGLU: within each wave's WTN(=64)-column slab, columns [0,32) are the value half and
     // [32,64) the gate half of output columns slab*32 + [0,32) (N % 128 == 0: always vector).
-    // (Launches with other wave widths never carry the GEGLU epilogue: launch_mode.)
+    // (Launches with other wave widths never carry the GEGLU epilogue: launch_mode.)  The bias
+    // vectors depend on the column only: loaded once, before the first use (p.C may alias p.bias
+    // as far as the compiler knows, so it would otherwise reload them per fragment behind a wait).
+    f32x4 bh[RN / 2], bg[RN / 2];
+#pragma unroll
+    for (int j = 0; j < RN / 2; ++j) {
+      const int nh = nw + j * 16 + fq * 4;
+      bh[j] = p.bias ? *(const f32x4*)(p.bias + nh) : f32x4{0.f, 0.f, 0.f, 0.f};
+      bg[j] = p.bias ? *(const f32x4*)(p.bias + nh + WTN / 2) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
       const int m = rows.row(i);
@@ -255,14 +264,12 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
       const long crow = cb + (long)m * p.ldc;
 #pragma unroll
       for (int j = 0; j < RN / 2; ++j) {
-        const int nh = nw + j * 16 + fq * 4;
-        const int ng = nh + WTN / 2;
         const int no = nw / 2 + j * 16 + fq * 4;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float h = acc[i][j][r] * p.alpha + (p.bias ? p.bias[nh + r] : 0.f);
-          const float g = acc[i][j + RN / 2][r] * p.alpha + (p.bias ? p.bias[ng + r] : 0.f);
+          const float h = acc[i][j][r] * p.alpha + bh[j][r];
+          const float g = acc[i][j + RN / 2][r] * p.alpha + bg[j][r];
           v[r] = h * gelu_erf(g);
           if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
         }
