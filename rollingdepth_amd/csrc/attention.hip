@@ -66,7 +66,8 @@ constexpr int NSLOT = 5;
 // Measured alternatives (tools/kbench.py, L0 shape, same process): issuing the DMA in the MFMA
 // block instead of the softmax block −4 %; packed v_pk_add_f32 row sums −11 %; no priority flips
 // (MFMA block pinned by sched_barrier) or a static s_setprio 1 for waves 4-7 instead: within ±2 %
-// run-to-run (profiles/r01_attn_prio_ab.log).
+// run-to-run (profiles/r01_attn_prio_ab.log); one row-sum partial per key block (4 independent
+// add chains instead of one) −11 %.
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   __shared__ __attribute__((aligned(16))) f16 lds[NSLOT * 2 * TILE];  // 160 KB: slot s = [K | V]
   const int tid = threadIdx.x;
