@@ -9,11 +9,13 @@
 //   lane-local plus one lane^32 exchange); Oᵀ = Vᵀ·Pᵀ with the P accumulator re-used directly
 //   as the B operand (keys in the MFMA's permuted k order) and V read from LDS with
 //   ds_read_b64_tr_b16 (hardware transpose).  Online softmax in exp2 domain with the running max
-//   folded into the QKᵀ MFMA chain (details at the kernel).
+//   entering the QKᵀ MFMA chain as its initial accumulator (details at the kernel).
 // attn_smallkv: attention of every query token against ≤ 16 shared keys (the UNet's
 //   cross-attention to the 2-token empty-text context) — a streaming kernel, no MFMA.
 // softmax_rows: f32 scores → f16 probabilities, for the d=C single-head VAE attention that is
 //   run as GEMM → softmax → GEMM.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -42,18 +44,20 @@ __device__ __forceinline__ void attn_wait_vmcnt() {
 // XOR-swizzled by (key & 7) through the per-lane source offset; V stays row-major for the
 // transposed reads.  Keys past Sk fall outside the buffer descriptors' range and read as zeros.
 //
-// Softmax VALU budget.  Q is prescaled by scale·log2(e) once, and the running row maximum m is
-// folded into the Sᵀ = K·Qᵀ MFMA chain as a 65th head dimension: K' = [K | 1], Q' = [Q | -m̃]
-// (one extra 32x32x16 MFMA per key block whose A operand is the constant "ones" column and whose
-// B operand carries -m̃ in f16), so the MFMA delivers S' = scores − m̃ directly and each score costs
-// only exp2, one add (row sum) and half a cvt_pk.  m̃ is kept as an f16 value (softmax is
-// shift-invariant, so any m̃ works as long as O and l share it).  It is set exactly on the first
-// tile and re-set — with the O/l rescale — only when a tile's row sum over this lane's 64 keys
-// exceeds 2^15 (the f16 range of P), i.e. when the row max grew by more than ≈9 (log2 units);
-// otherwise P stays bounded by 2^15 and f16 P keeps its relative precision.
-//
+// Softmax VALU budget.  Q is prescaled by scale·log2(e) once, and the running row maximum m̃ enters
+// the Sᵀ = K·Qᵀ MFMA chain as its initial accumulator (-m̃ in all 16 entries of a lane: in the swapped
+// layout a lane's accumulator entries all belong to its one query), so the chain delivers
+// S' = scores − m̃ directly and each score costs only exp2, half a cvt_pk and half a packed f16 add
+// (the row sum is a pairwise v_pk_add_f16 tree over the f16 P the PV MFMA consumes).  The
+// rescale is rare: m̃ is set exactly on the first tile and re-set — with the O/l rescale — only
+// when a tile's row sum over this lane's 64 keys exceeds 2^15 (the f16 range of P), i.e. when
+// the row max grew by more than ≈9 (log2 units); otherwise P stays bounded by 2^15 and f16 P keeps
+// its relative precision.  (Earlier form: m̃ as a 65th head dimension, K' = [K | 1], Q' = [Q | -m̃],
+// one extra MFMA per 32-key block: 3 % slower than the accumulator init; f32 v_add row sums: 4 %
+// slower than the f16 tree — tools/kbench.py attn, RDMI_ATTN_F32SUM=1 selects the f32 sums.)
+
 // MFMA/VALU overlap.  Per tile t a wave runs an MFMA block M(t) = {Oᵀ += Vᵀ·P(t-1)ᵀ; S'(t) =
-// K'(t)·Q'ᵀ} (36 MFMAs) and a VALU block S(t) = {softmax of S'(t) → P(t); DMA}, separated by
+// K(t)·Qᵀ − m̃} (32 MFMAs) and a VALU block S(t) = {softmax of S'(t) → P(t); DMA}, separated by
 // barriers.  Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave is in its MFMA
 // block while its partner is in its VALU block (guide §5.5 T16 / MI355X_MICROARCH "Two waves per
 // SIMD").  With interval i between barriers, group g runs M(t) in interval 2t+g and S(t) in
@@ -68,6 +72,7 @@ constexpr int NSLOT = 5;
 // (MFMA block pinned by sched_barrier) or a static s_setprio 1 for waves 4-7 instead: within ±2 %
 // run-to-run (profiles/r01_attn_prio_ab.log); one row-sum partial per key block (4 independent
 // add chains instead of one) −11 %.
+template <bool F16SUM>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   __shared__ __attribute__((aligned(16))) f16 lds[NSLOT * 2 * TILE];  // 160 KB: slot s = [K | V]
   const int tid = threadIdx.x;
@@ -96,8 +101,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     qf[ks] *= qs;
   }
   // the 65th dimension: A = ones column (k index 0 of the lanes < 32), B = -m̃ (same slot)
-  f16x8 ones = {}, qaug = {};
-  if (hh == 0) ones[0] = (f16)1.f;
+  // -m̃ enters as the chain's initial accumulator (rows are lane-local in the swapped layout, so all
+  // 16 accumulator entries of a lane carry its query's -m̃)
+  f32x16 negm = {};
 
   // DMA lane geometry: 8 rows x 8 chunks per 1-KiB instruction; row = (i*NWV + wid)*8 + drow.
   // LDS images (bank-conflict-free for the fragment reads, checked with SQ_LDS_BANK_CONFLICT):
@@ -138,7 +144,6 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   const int gi = lane >> 4, li = lane & 15;
   const int tr_key = 4 * (gi >> 1) + (li >> 2);
   const int tr_col = 16 * (gi & 1) + 4 * (li & 3);
-  const f32x16 zero16 = {};
   f16x8 pf[2 * NKB] = {};
 
   // Oᵀ += Vᵀ · Pᵀ for the tile in slot `slot` (KB/16 k-steps of 16 keys, 2 d-blocks of 32).
@@ -187,6 +192,19 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     }
   };
 
+  // Row sum of this lane's 64 probabilities as the MFMA will see them (the f16 P): a pairwise tree
+  // of packed f16 adds (31 v_pk_add_f16 instead of 64 v_add_f32 on the softmax's VALU critical
+  // path).  Partial sums stay ≤ the 2^15 rescale bound (an overflow to inf triggers the rescale).
+  auto psum = [&]() -> float {
+    f16x8 a0 = pf[0] + pf[1], a1 = pf[2] + pf[3], a2 = pf[4] + pf[5], a3 = pf[6] + pf[7];
+    a0 += a1;
+    a2 += a3;
+    a0 += a2;
+    f16x4 b = __builtin_shufflevector(a0, a0, 0, 1, 2, 3) + __builtin_shufflevector(a0, a0, 4, 5, 6, 7);
+    f16x2 c2 = __builtin_shufflevector(b, b, 0, 1) + __builtin_shufflevector(b, b, 2, 3);
+    return (float)c2[0] + (float)c2[1];
+  };
+
   // prologue: DMA(0..2) issued ("S(-3..-1)"), DMA(0) and DMA(1) waited ("S(-2), S(-1)")
   issue(0);
   issue(1);
@@ -211,10 +229,8 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
       for (int ks = 0; ks < 4; ++ks) {
         const int ch = 2 * ks + hh;
         f16x8 kf = *(const f16x8*)(ks_ + key * 64 + ((ch ^ ((key >> 1) & 7)) << 3));
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], ks ? s[kb] : zero16, 0, 0, 0);
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], ks ? s[kb] : negm, 0, 0, 0);
       }
-      // last in the chain (a distinct accumulator input per block: no CSE into register copies)
-      s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ones, qaug, s[kb], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
     asm volatile("" ::: "memory");
@@ -240,9 +256,10 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float e = __builtin_amdgcn_exp2f(s[kb][r]);  // v_exp_f32, no denorm fixup
-        rs += e;
+        if (!F16SUM) rs += e;
         pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
       }
+    if (F16SUM) rs = psum();
     // ---- (re)set m̃: always on the first tile, else only when P would leave the f16 range
     if (kt == 0 || __any(!(rs <= 32768.f))) {
       float mx = -INFINITY;
@@ -261,16 +278,18 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
       mt = mnew;
-      qaug[0] = hh == 0 ? (f16)(-mnew) : (f16)0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) negm[r] = -mnew;
       rs = 0.f;
 #pragma unroll
       for (int kb = 0; kb < NKB; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float e = __builtin_amdgcn_exp2f(s[kb][r] - delta);
-          rs += e;
+          if (!F16SUM) rs += e;
           pf[kb * 2 + (r >> 3)][r & 7] = (f16)e;
         }
+      if (F16SUM) rs = psum();
     }
     l += rs;
     attn_wait_vmcnt<2 * DPW>();  // DMA(kt+2) landed (DMA(kt+3) in flight)
@@ -447,7 +466,11 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
   AttnP p{(const f16*)q, (const f16*)k, (const f16*)v, (f16*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs,
           scale * 1.4426950408889634f};
   dim3 g(rdmi::div_up(Sq, QB), H, B);
-  hipLaunchKernelGGL(attn_fwd_d64, g, dim3(64 * NWV), 0, (hipStream_t)stream, p);
+  static const bool f32sum = [] { const char* e = getenv("RDMI_ATTN_F32SUM"); return e && e[0] == '1'; }();
+  if (!f32sum)
+    hipLaunchKernelGGL(attn_fwd_d64<true>, g, dim3(64 * NWV), 0, (hipStream_t)stream, p);
+  else
+    hipLaunchKernelGGL(attn_fwd_d64<false>, g, dim3(64 * NWV), 0, (hipStream_t)stream, p);
   return rdmi::check_launch("attention_fwd");
 }
 
