@@ -143,9 +143,31 @@ __global__ void snippet_average_k(const f16* __restrict__ src, int n, int w, int
   }
 }
 
-__global__ void minmax_partial(const void* __restrict__ x, int xf32, long n, float* __restrict__ part) {
+// 16-B vector loads (8 halves / 4 floats per lane and step), scalar tail; min/max are
+// order-independent, so the result is exact whatever the split.
+__global__ __launch_bounds__(256) void minmax_partial(const void* __restrict__ x, int xf32, long n,
+                                                      float* __restrict__ part) {
   float mn = INFINITY, mx = -INFINITY;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long t0 = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const bool al = ((uintptr_t)x & 15) == 0;
+  const int per = xf32 ? 4 : 8;
+  const long nvec = al ? n / per : 0;
+  for (long i = t0; i < nvec; i += stride) {
+    if (xf32) {
+      const f32x4 v = ((const f32x4*)x)[i];
+      mn = fminf(mn, fminf(fminf(v[0], v[1]), fminf(v[2], v[3])));
+      mx = fmaxf(mx, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    } else {
+      const f16x8 v = ((const f16x8*)x)[i];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        mn = fminf(mn, (float)v[e]);
+        mx = fmaxf(mx, (float)v[e]);
+      }
+    }
+  }
+  for (long i = nvec * per + t0; i < n; i += stride) {
     float v = xf32 ? ((const float*)x)[i] : (float)((const f16*)x)[i];
     mn = fminf(mn, v);
     mx = fmaxf(mx, v);
@@ -256,8 +278,8 @@ extern "C" int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long l
 
 extern "C" int rdmi_minmax(const void* x, int x_f32, long n, float* minmax, float* workspace, void* stream) {
   RDMI_REQUIRE(x && minmax && workspace && n > 0, RDMI_E_ARG, "minmax: bad args");
-  unsigned g = grid_for(n);
-  if (g > 1024) g = 1024;
+  unsigned g = grid_for((n + 7) / 8);
+  if (g > 2048) g = 2048;
   hipLaunchKernelGGL(minmax_partial, dim3(g), dim3(256), 0, (hipStream_t)stream, x, x_f32, n, workspace);
   int rc = rdmi::check_launch("minmax_partial");
   if (rc) return rc;

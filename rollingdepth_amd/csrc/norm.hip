@@ -126,11 +126,22 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
   const long total = nv * nb;
   const float* base = part + (long)(g * nv) * ld + (long)b * nb * 2;
   double S = 0.0, SS = 0.0;
-  for (long i = t; i < total; i += 256) {
-    const long v = i / nb, k = i - v * nb;
-    const float* e = base + v * ld + k * 2;
-    S += (double)e[0];
-    SS += (double)e[1];
+  // 8 independent loads in flight per thread, summed in the same per-thread order as one at a time
+  constexpr int U = 8;
+  for (long i0 = t; i0 < total; i0 += 256 * U) {
+    f32x2 e[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long i = i0 + 256 * j;
+      const long v = i / nb, k = i - v * nb;
+      e[j] = i < total ? *(const f32x2*)(base + v * ld + k * 2) : f32x2{0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (i0 + 256 * j < total) {
+        S += (double)e[j][0];
+        SS += (double)e[j][1];
+      }
   }
   __shared__ double rs[256], rq[256];
   rs[t] = S;
