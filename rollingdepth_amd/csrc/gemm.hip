@@ -32,6 +32,7 @@ struct GemmP {
   int group_m;  // tile order inside an XCD's range: groups of group_m m-tiles, n-tiles within a group
   // GroupNorm (+SiLU) of the conv INPUT, applied as it is read (conv_halo_kernel<..., GN = true>)
   const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
+  int gelu_exact;  // GEGLU through ocml erff instead of gelu_erf_fast (RDMI_GELU_EXACT=1, A/B)
 };
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
@@ -270,7 +271,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
         for (int r = 0; r < 4; ++r) {
           const float h = acc[i][j][r] * p.alpha + bh[j][r];
           const float g = acc[i][j + RN / 2][r] * p.alpha + bg[j][r];
-          v[r] = h * gelu_erf(g);
+          v[r] = h * (p.gelu_exact ? gelu_erf(g) : gelu_erf_fast(g));
           if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
         }
         if (p.c_f32) {
@@ -1492,6 +1493,10 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.alpha = a->alpha;
   p.M = a->M; p.N = a->N; p.K = (a->K + BK - 1) / BK * BK; p.Kvalid = a->K;
   p.geglu = a->epilogue == RDMI_EPI_GEGLU;
+  if (p.geglu) {
+    const char* ge = getenv("RDMI_GELU_EXACT");
+    p.gelu_exact = ge && ge[0] == '1';
+  }
   p.silu = a->epilogue == RDMI_EPI_SILU;
   p.vec = vec_ok(p);
   RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm: GEGLU output needs 4-element aligned rows");
