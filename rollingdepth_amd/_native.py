@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "librdmi.so")
+_LIB_PATH = os.environ.get("RDMI_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "librdmi.so")
 
 vp = C.c_void_p
 i32 = C.c_int

@@ -189,6 +189,18 @@ def bench_host(iters):
         print(f"host  {lab:32s} {dt * 1e6:9.1f} us per call")
 
 
+def bench_aligner(iters):
+    """DepthAligner.run at the fast preset (N=100, dilations [1, 25], 768², 2000 iterations)."""
+    from rollingdepth_amd import DepthAligner
+    g = torch.Generator(device="cuda").manual_seed(0)
+    sn = [(torch.rand(n, 3, 1, 768, 768, device="cuda", generator=g) * 0.8 + 0.1).half() for n in (98, 50)]
+    al = DepthAligner("cuda")
+    al.run(sn, [1, 25])
+    torch.cuda.synchronize()
+    ms = timeit(lambda: al.run(sn, [1, 25]), max(1, iters // 10))
+    print(f"aligner fast preset N=100 2000 it        {ms * 1e3:9.1f} us")
+
+
 def bench_attn(iters):
     for lab, B, S, H in [("L0 S=27648 H=5 b=8", 8, 27648, 5), ("L1 S=6912 H=10 b=8", 8, 6912, 10),
                          ("L2 S=1728 H=20 b=8", 8, 1728, 20), ("mid S=432 H=20 b=8", 8, 432, 20)]:
@@ -225,4 +237,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host}[part](a.iters)
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner}[part](a.iters)
