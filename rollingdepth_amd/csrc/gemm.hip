@@ -32,6 +32,7 @@ struct GemmP {
   int group_m;  // tile order inside an XCD's range: groups of group_m m-tiles, n-tiles within a group
   // GroupNorm (+SiLU) of the conv INPUT, applied as it is read (conv_halo_kernel<..., GN = true>)
   const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
+  int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
   int gelu_exact;  // GEGLU through ocml erff instead of gelu_erf_fast (RDMI_GELU_EXACT=1, A/B)
 };
 
@@ -92,9 +93,23 @@ struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; H
   __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }  // conv: rpg = Ho·Wo
 };
 
+// 16-B epilogue accesses for the halo convs (p.cperm).  The weight rows are DMA'd into LDS in a
+// permuted order (perm64 within each wave's 64-channel slab) so that MFMA fragments 2q and 2q+1
+// of a lane hold 8 CONSECUTIVE output channels: fragment j, channel slot fq*4 + r lands on channel
+// 32(j/2) + 8fq + 4(j%2) + r.  The epilogue then loads residuals and stores outputs as 16-B
+// vectors (half the address-processing work of the 8-B per-fragment accesses); the K order per
+// output element is unchanged, so the results are bitwise those of the unpermuted kernel.
+__device__ __forceinline__ int perm64(int r) {
+  const int j = r >> 4, c = r & 15;
+  return 32 * (j >> 1) + 8 * (c >> 2) + 4 * (j & 1) + (c & 3);
+}
+__device__ __forceinline__ int col_base(bool perm, int nw, int j, int fq) {
+  return perm ? nw + 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : nw + j * 16 + fq * 4;
+}
+
 template <int RM, int RN, int WTN, class Rows>
 __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
-                                           int fr, int fq) {
+                                           int fr, int fq, bool perm = false) {
   const long cb = (long)bz * p.sC;
   const long rbz = (long)bz * p.sR;
   // Fast path for whole f16 tiles (every row exists, every 4-column group inside N, one row-bias
@@ -105,25 +120,36 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
     f32x4 badd[RN];
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
-      const int n = nw + j * 16 + fq * 4;
+      const int n = col_base(perm, nw, j, fq);
       badd[j] = p.bias ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
       if (p.rowbias) badd[j] += *(const f32x4*)(p.rowbias + (long)rbg * p.rb_ld + n);
     }
     f16x4 rr[RM][RN];
     if (p.R) {
 #pragma unroll
-      for (int i = 0; i < RM; ++i)
+      for (int i = 0; i < RM; ++i) {
+        const f16* rrow = p.R + rbz + (long)rows.row(i) * p.ldr;
+        if (perm && RN % 2 == 0) {
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          rr[i][j] = *(const f16x4*)(p.R + rbz + (long)rows.row(i) * p.ldr + nw + j * 16 + fq * 4);
+          for (int j = 0; j < RN; j += 2) {
+            const f16x8 v = *(const f16x8*)(rrow + col_base(true, nw, j, fq));
+            rr[i][j] = __builtin_shufflevector(v, v, 0, 1, 2, 3);
+            rr[i][j + 1] = __builtin_shufflevector(v, v, 4, 5, 6, 7);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < RN; ++j) rr[i][j] = *(const f16x4*)(rrow + col_base(false, nw, j, fq));
+        }
+      }
     }
     float gs[RN], gq[RN];
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
       const long crow = cb + (long)rows.row(i) * p.ldc;
+      f16x4 ov[RN];
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        const int n = nw + j * 16 + fq * 4;
+        const int n = col_base(perm, nw, j, fq);
         f16x4 o;
         float s = 0.f, q = 0.f;
 #pragma unroll
@@ -136,7 +162,11 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
           s += f;
           q = fmaf(f, f, q);
         }
-        *(f16x4*)((f16*)p.C + crow + n) = o;
+        ov[j] = o;
+        if (!(perm && RN % 2 == 0)) *(f16x4*)((f16*)p.C + crow + n) = o;
+        else if (j & 1)
+          *(f16x8*)((f16*)p.C + crow + col_base(true, nw, j - 1, fq)) =
+              __builtin_shufflevector(ov[j - 1], o, 0, 1, 2, 3, 4, 5, 6, 7);
         if (p.gnp) {  // as below: fixed butterfly over the 16 rows of the fragment pair
           if (!(i & 1)) {
             gs[j] = s;
@@ -169,7 +199,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
       const long rrow = rbz + (long)m * p.ldr;
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        const int n = nw + j * 16 + fq * 4;
+        const int n = col_base(perm, nw, j, fq);
         const bool ok = mok && n < p.N;
         float s = 0.f, q = 0.f;
         if (ok) {
@@ -835,7 +865,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   int brow[NB];
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
-    const int n = n0 + (wid + 8 * e) * 8 + lrow;
+    const int rt = (wid + 8 * e) * 8 + lrow;  // LDS row of the tile
+    const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
     brow[e] = n < p.N ? n * (int)p.ldw : -1;
   }
   const int ncb = p.Cin >> 6;
@@ -1029,7 +1060,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   if (grp == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq);
+  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
 }
 
 // Two-workgroups-per-CU halo conv for 128-channel output tiles (the VAE's 768² convs).  With
@@ -1095,7 +1126,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   int brow[NB];
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
-    const int n = n0 + (wid + 4 * e) * 8 + lrow;
+    const int rt = (wid + 4 * e) * 8 + lrow;  // LDS row of the tile
+    const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
     brow[e] = n < p.N ? n * (int)p.ldw : -1;
   }
   const int ncb = p.Cin >> 6;
@@ -1224,7 +1256,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
   }
-  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq);
+  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
 }
 
 // Two-workgroups-per-CU dense GEMM (the UNet's single-batch Linears).  A 256×256
@@ -1549,6 +1581,9 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   if (halo_eligible(a, hmode)) {
     const char* gm = getenv("RDMI_GEMM_GROUP");
     p.group_m = gm ? atoi(gm) : 8;
+    const char* cp = getenv("RDMI_CPERM");
+    p.cperm = (!cp || cp[0] != '0') && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 &&
+              (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0));
     p.gmr = a->in_mean_rstd; p.ggam = a->in_gamma; p.gbet = a->in_beta; p.gG = a->in_groups; p.gsilu = a->in_silu;
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
