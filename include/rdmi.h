@@ -146,6 +146,15 @@ int rdmi_attention_smallkv(const void* q, const void* k, const void* v, void* o,
                            int Sq, int L, int D, long q_ld, long o_ld, long q_bs, long o_bs,
                            long kv_bs, float scale, void* stream);
 
+/* BasicTransformerBlock's norm2 → attn2 → +residual against a TWO-token shared context
+ * (attention.py:480-492, attention_processor.py:2172-2276 with Sk = 2), collapsed by exact algebra:
+ * y = x + c + Σ_h σ(LN(x)·w_h) u_h with w = scale·Wq_hᵀ(K1−K0)_h and u_h = Wo_h(V1−V0)_h
+ * ([H, C] f32 each, 16-B aligned), c = Wo·V0 + bo ([C] f32).  x, y: [M, C] f16 rows (C ≤ 1536,
+ * 2·H·C·4 B ≤ 64 KiB).  Replaces LN + q GEMM + rdmi_attention_smallkv + out GEMM for that case. */
+int rdmi_cross_attn_pair(const void* x, void* y, long M, int C, int H, const float* ln_gamma,
+                         const float* ln_beta, float eps, const float* w, const float* u, const float* c,
+                         void* stream);
+
 /* Row softmax: p[r, :] = softmax(scale * s[r, :]) (f32 in, f16 out).  Used with two rdmi_gemm
  * calls for the single-head d=C VAE mid-block attention (unet_2d_blocks.py:680-697). */
 /* p[r·p_ld + c] = softmax_c(scale·s[r·cols + c]) for c < cols, 0 for cols ≤ c < p_ld (so a PV GEMM

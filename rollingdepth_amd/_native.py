@@ -75,6 +75,7 @@ _SIGS = {
     "rdmi_attention_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i64, i64, i64,
                                  f32, vp]),
     "rdmi_attention_smallkv": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, f32, vp]),
+    "rdmi_cross_attn_pair": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, vp, vp, vp]),
     "rdmi_softmax_rows": (i32, [vp, vp, i64, i64, i64, f32, vp]),
     "rdmi_nchw_to_nhwc": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, f32, i64, i64, vp]),
     "rdmi_nhwc_to_nchw_f32": (i32, [vp, i64, vp, i32, i32, i32, i32, f32, f32, vp]),

@@ -453,6 +453,124 @@ __global__ __launch_bounds__(256) void softmax_rows_reg_k(const float* __restric
   for (long c = cols + threadIdx.x; c < p_ld; c += 256) pr[c] = (f16)0.f;  // K padding of the PV GEMM
 }
 
+// attn2 block against a TWO-token context (the empty-text embedding BOS+EOS), collapsed by exact
+// algebra (attention_processor.py:2172-2276 with Sk = 2; attention.py:480-492 norm2 + residual):
+// softmax over two keys is σ(s1 − s0), so per head h
+//   o_h = V0_h + σ(n2·w_h) (V1_h − V0_h),  w_h = scale · Wq_hᵀ (K1_h − K0_h)
+// and after to_out: out = t + c + Σ_h σ(n2·w_h) u_h,  u_h = Wo_h (V1_h − V0_h),  c = Wo V0 + bo,
+// with n2 = LayerNorm(t) (norm2, rounded to f16 as the unfused LN output).  One wave per token
+// row: LN moments (same order as layernorm_k), H dot products against w (LDS), the sigmoid
+// weights, the output row — one read and one write of the row instead of LN + q GEMM + attention
+// + out GEMM (five row passes).  w, u, c are folded once per context (unet.Transformer).
+template <int NV>  // f16x8 vectors per lane: C ≤ 512·NV
+__global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f16* __restrict__ y, long M, int C,
+                                                    int H, const float* __restrict__ g, const float* __restrict__ b,
+                                                    float eps, const float* __restrict__ wd,
+                                                    const float* __restrict__ u, const float* __restrict__ c0) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // w [H][C] | u [H][C]
+  for (int i = threadIdx.x; i < H * C / 4; i += 256) {
+    ((f32x4*)sm)[i] = ((const f32x4*)wd)[i];
+    ((f32x4*)sm)[H * C / 4 + i] = ((const f32x4*)u)[i];
+  }
+  __syncthreads();
+  const float* ws = sm;
+  const float* us = sm + H * C;
+  const int lane = threadIdx.x & 63;
+  const int CV = C >> 3;
+  // this lane's columns are fixed: LN affine and the constant row c stay in registers
+  float gr[NV][8], br[NV][8], cr[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int cv = lane + 64 * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int cc = cv < CV ? cv * 8 + e : 0;
+      gr[i][e] = g[cc];
+      br[i][e] = b[cc];
+      cr[i][e] = c0[cc];
+    }
+  }
+  const long stride = gridDim.x * 4L;
+  long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  f16x8 vn[NV];  // next row, loaded one row ahead
+  auto load = [&](long r) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int cv = lane + 64 * i;
+      if (r < M && cv < CV) vn[i] = *(const f16x8*)(x + r * C + cv * 8);
+    }
+  };
+  load(row);
+  for (; row < M; row += stride) {
+    f16x8 v[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = vn[i];
+    load(row + stride);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (lane + 64 * i < CV)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)v[i][e];
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (lane + 64 * i < CV)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = (float)v[i][e] - mean;
+          q += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(q) / C + eps);
+    float n[NV][8], o[NV][8];
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        n[i][e] = lane + 64 * i < CV ? (float)(f16)(((float)v[i][e] - mean) * rstd * gr[i][e] + br[i][e]) : 0.f;
+        o[i][e] = 0.f;
+      }
+    for (int h = 0; h < H; ++h) {
+      float d = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int cv = lane + 64 * i;
+        if (cv < CV) {
+          const f32x4 w0 = *(const f32x4*)(ws + h * C + cv * 8), w1 = *(const f32x4*)(ws + h * C + cv * 8 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d = fmaf(n[i][e], w0[e], fmaf(n[i][4 + e], w1[e], d));
+        }
+      }
+      d = wave_sum(d);
+      const float ph = 1.0f / (1.0f + __expf(-d));
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int cv = lane + 64 * i;
+        if (cv < CV) {
+          const f32x4 u0 = *(const f32x4*)(us + h * C + cv * 8), u1 = *(const f32x4*)(us + h * C + cv * 8 + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[i][e] = fmaf(ph, u0[e], o[i][e]);
+            o[i][4 + e] = fmaf(ph, u1[e], o[i][4 + e]);
+          }
+        }
+      }
+    }
+    f16* yr = y + row * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int cv = lane + 64 * i;
+      if (cv < CV) {
+        f16x8 r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = (f16)((float)v[i][e] + (cr[i][e] + o[i][e]));
+        *(f16x8*)(yr + cv * 8) = r;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
@@ -499,4 +617,29 @@ extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, 
   else
     hipLaunchKernelGGL(softmax_rows_k, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
   return rdmi::check_launch("softmax_rows");
+}
+
+extern "C" int rdmi_cross_attn_pair(const void* x, void* y, long M, int C, int H, const float* ln_gamma,
+                                    const float* ln_beta, float eps, const float* w, const float* u, const float* c,
+                                    void* stream) {
+  RDMI_REQUIRE(x && y && ln_gamma && ln_beta && w && u && c && M > 0 && H > 0, RDMI_E_ARG, "cross_attn_pair: bad args");
+  RDMI_REQUIRE(C % 8 == 0 && C <= 64 * 8 * 3, RDMI_E_UNSUPPORTED, "cross_attn_pair: C=%d unsupported", C);
+  RDMI_REQUIRE((((uintptr_t)x | (uintptr_t)y | (uintptr_t)w | (uintptr_t)u) & 15) == 0, RDMI_E_ALIGN,
+               "cross_attn_pair: pointers must be 16-byte aligned");
+  const size_t lds = (size_t)2 * H * C * sizeof(float);
+  RDMI_REQUIRE(lds <= 64 * 1024 && H <= 16, RDMI_E_UNSUPPORTED, "cross_attn_pair: H=%d, H*C=%d unsupported", H, H * C);
+  long blocks = (M + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  const int nv = (C / 8 + 63) / 64;
+#define RDMI_PAIR(NVV) \
+  hipLaunchKernelGGL(attn2_pair_k<NVV>, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, (const f16*)x, \
+                     (f16*)y, M, C, H, ln_gamma, ln_beta, eps, w, u, c)
+  if (nv == 1)
+    RDMI_PAIR(1);
+  else if (nv == 2)
+    RDMI_PAIR(2);
+  else
+    RDMI_PAIR(3);
+#undef RDMI_PAIR
+  return rdmi::check_launch("cross_attn_pair");
 }

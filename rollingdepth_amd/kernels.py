@@ -402,6 +402,35 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
     return out
 
 
+def fold_attn2_pair(wq: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, k2: torch.Tensor, v2: torch.Tensor,
+                    heads: int):
+    """Once-per-context fold for rdmi_cross_attn_pair (weight folding, like packing): wq/wo [C, C]
+    f32 (f16-rounded to_q / to_out weights), bo [C], k2/v2 [2, C] the projected context keys /
+    values → (w [H, C], u [H, C], c [C]) f32 with w_h = Wq_hᵀ(k1−k0)_h/√d, u_h = Wo_h(v1−v0)_h,
+    c = Wo·v0 + bo."""
+    C_ = wq.shape[1]
+    d = C_ // heads
+    k, v = k2.float(), v2.float()
+    dk, dv = (k[1] - k[0]).view(heads, d, 1), (v[1] - v[0]).view(1, heads, d)
+    w = (dk * wq.view(heads, d, C_)).sum(1) / math.sqrt(d)
+    u = (dv * wo.view(-1, heads, d)).sum(2).t()
+    c = wo @ v[0] + bo
+    return w.contiguous(), u.contiguous(), c.contiguous()
+
+
+def cross_attn_pair(x: torch.Tensor, ln_g: torch.Tensor, ln_b: torch.Tensor, eps: float, w: torch.Tensor,
+                    u: torch.Tensor, c: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [M, C] f16 → x + c + Σ_h σ(LN(x)·w_h) u_h (attn2 against a two-token context, rdmi.h)."""
+    _need(x, F16, "cross_attn_pair.x")
+    M, C_ = x.shape
+    H = w.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    check(lib.rdmi_cross_attn_pair(x.data_ptr(), out.data_ptr(), M, C_, H, ln_g.data_ptr(), ln_b.data_ptr(), eps,
+                                   w.data_ptr(), u.data_ptr(), c.data_ptr(), _stream()), "rdmi_cross_attn_pair")
+    return out
+
+
 def attention_smallkv(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [B, Sq, H*64] (row stride any), k/v [Bkv, L, H*64] contiguous with Bkv ∈ {1, B}."""

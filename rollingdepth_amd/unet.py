@@ -15,6 +15,7 @@ cross-frame fold, attention_processor.py:2208-2266).  Weights come from a diffus
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -124,6 +125,14 @@ class Transformer:
         self.ff1_b = bp.to(dev, F32)
         self.ff2 = _Lin(sd, q + ".ff.net.2", dev)
         self._ctx_key = None
+        # f16-rounded to_q / to_out weights for the two-token attn2 fold (set_context), kept only where
+        # the folded [H, C] w / u tables fit the kernel's LDS (2·H·C·4 B ≤ 64 KiB, H ≤ 16: C ≤ 640 at d = 64)
+        self._pair = None
+        self._pair_w = None
+        if 2 * heads * self.c * 4 <= 64 * 1024 and heads <= 16 and os.environ.get("RDMI_ATTN2_PAIR", "1") != "0":
+            self._pair_w = (sd[q + ".attn2.to_q.weight"].half().float().to(dev),
+                            sd[q + ".attn2.to_out.0.weight"].half().float().to(dev),
+                            sd.get(q + ".attn2.to_out.0.bias", torch.zeros(self.c)).float().to(dev))
 
     def set_context(self, ctx16: torch.Tensor):
         """K/V of attn2 for the (constant) encoder_hidden_states [Bc, L, Dctx] f16."""
@@ -132,6 +141,10 @@ class Transformer:
         self.k2c = K.gemm(ctx16, self.k2.w, self.k2.k)
         self.v2c = K.gemm(ctx16, self.v2.w, self.v2.k)
         self._ctx_key = ctx16
+        self._pair = None
+        if self._pair_w is not None and self.k2c.shape[0] == 1 and self.k2c.shape[1] == 2:
+            # exact fold of softmax over two keys (attention.hip attn2_pair_k): once per context
+            self._pair = K.fold_attn2_pair(*self._pair_w, self.k2c[0], self.v2c[0], self.heads)
 
     def __call__(self, x, num_view: Optional[int]):
         B, H, W, C = x.shape
@@ -147,14 +160,17 @@ class Transformer:
         o = K.attention(qkv3[..., :C], qkv3[..., C:2 * C], qkv3[..., 2 * C:], self.heads)
         t = self.o1(o.view(B * HW, C), residual=t)
         # attn2: cross-attention to the context (the fold is a no-op for shared K/V)
-        n2 = K.layernorm(t, self.ln2.g, self.ln2.b, 1e-5)
-        q2 = self.q2(n2)
-        kv_b = self.k2c.shape[0]
-        if kv_b == 1:
-            o2 = K.attention_smallkv(q2.view(1, B * HW, C), self.k2c, self.v2c, self.heads)
+        if self._pair is not None:  # two-token context: norm2 + attn2 + residual in one row pass
+            t = K.cross_attn_pair(t, self.ln2.g, self.ln2.b, 1e-5, *self._pair)
         else:
-            o2 = K.attention_smallkv(q2.view(kv_b, -1, C), self.k2c, self.v2c, self.heads)
-        t = self.o2(o2.view(B * HW, C), residual=t)
+            n2 = K.layernorm(t, self.ln2.g, self.ln2.b, 1e-5)
+            q2 = self.q2(n2)
+            kv_b = self.k2c.shape[0]
+            if kv_b == 1:
+                o2 = K.attention_smallkv(q2.view(1, B * HW, C), self.k2c, self.v2c, self.heads)
+            else:
+                o2 = K.attention_smallkv(q2.view(kv_b, -1, C), self.k2c, self.v2c, self.heads)
+            t = self.o2(o2.view(B * HW, C), residual=t)
         # GEGLU feed-forward
         n3 = K.layernorm(t, self.ln3.g, self.ln3.b, 1e-5)
         f = K.gemm(n3, self.ff1_w, C, bias=self.ff1_b, geglu=True)

@@ -367,6 +367,29 @@ def test_attention_smallkv():
     assert (o.float() - ref).abs().max().item() < 3e-3
 
 
+@pytest.mark.parametrize("M,C,H", [(999, 320, 5), (517, 640, 10), (64, 128, 2)])
+def test_cross_attn_pair(M, C, H):
+    """norm2 → attn2 (two-token context) → +residual as one row pass (rdmi_cross_attn_pair, exact
+    fold of the two-key softmax) against the unfolded fp32 computation of the reference block."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(31)
+    x = torch.randn(M, C, device=DEV, generator=g).half()
+    lg = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
+    lb = 0.1 * torch.randn(C, device=DEV, generator=g)
+    wq, wk, wv, wo = (torch.randn(C, C, device=DEV, generator=g) / math.sqrt(C) for _ in range(4))
+    wq, wo = wq.half().float(), wo.half().float()
+    bo = 0.1 * torch.randn(C, device=DEV, generator=g)
+    ctx = torch.randn(2, C, device=DEV, generator=g).half()
+    k2 = (ctx.float() @ wk.half().float().t()).half()
+    v2 = (ctx.float() @ wv.half().float().t()).half()
+    y = K_.cross_attn_pair(x, lg, lb, 1e-5, *K_.fold_attn2_pair(wq, wo, bo, k2, v2, H))
+    n2 = F.layer_norm(x.float(), (C,), lg, lb, 1e-5)
+    q = n2 @ wq.t()
+    o = _sdpa_ref(q.half()[None], k2[None], v2[None], H)[0]
+    ref = x.float() + o.float() @ wo.t() + bo
+    assert _rel(y, ref) < 4e-3
+
+
 @pytest.mark.parametrize("cols,pad", [(9216, 0), (5000, 8), (20000, 0), (1024, 0), (234, 6), (36, 4)])
 def test_softmax_rows(cols, pad):
     """Row softmax (single-pass register kernel for cols % 4 == 0 and ≤ 16384, three-pass

@@ -201,6 +201,30 @@ def bench_aligner(iters):
     print(f"aligner fast preset N=100 2000 it        {ms * 1e3:9.1f} us")
 
 
+def bench_pair(iters):
+    """norm2 → attn2 (two-token context) → +residual: fused row pass vs LN + q GEMM + attention + out GEMM."""
+    for lab, M, C, H in [("L0 25 snippets", 691200, 320, 5), ("L1 25 snippets", 172800, 640, 10)]:
+        x = torch.randn(M, C, device="cuda").half()
+        lg, lb = torch.ones(C, device="cuda"), torch.zeros(C, device="cuda")
+        wq, wo = (torch.randn(C, C, device="cuda") / math.sqrt(C) for _ in range(2))
+        bo = torch.zeros(C, device="cuda")
+        k2, v2 = torch.randn(2, C, device="cuda").half(), torch.randn(2, C, device="cuda").half()
+        fold = K.fold_attn2_pair(wq, wo, bo, k2, v2, H)
+        out = torch.empty_like(x)
+        ms_f = timeit(lambda: K.cross_attn_pair(x, lg, lb, 1e-5, *fold, out=out), iters)
+        wqp, wop = K.pack_linear(wq, "cuda"), K.pack_linear(wo, "cuda")
+
+        def unfused():
+            n2 = K.layernorm(x, lg, lb, 1e-5)
+            q = K.gemm(n2, wqp, C)
+            o = K.attention_smallkv(q.view(1, M, C), k2[None], v2[None], H)
+            K.gemm(o.view(M, C), wop, C, bias=bo, residual=x, out=out)
+
+        ms_u = timeit(unfused, iters)
+        print(f"pair  {lab:32s} fused {ms_f * 1e3:9.1f} us  unfused {ms_u * 1e3:9.1f} us  "
+              f"({4 * M * C / ms_f / 1e6:6.0f} GB/s row traffic)")
+
+
 def bench_attn(iters):
     for lab, B, S, H in [("L0 S=27648 H=5 b=8", 8, 27648, 5), ("L1 S=6912 H=10 b=8", 8, 6912, 10),
                          ("L2 S=1728 H=20 b=8", 8, 1728, 20), ("mid S=432 H=20 b=8", 8, 432, 20)]:
@@ -237,4 +261,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner}[part](a.iters)
+        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
