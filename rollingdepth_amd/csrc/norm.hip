@@ -216,50 +216,67 @@ __global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* 
 }
 
 // one wave per row; C ≤ 64*8*4 = 2048
+// One wave per row, grid-stride over rows: the lane's columns are fixed, so gamma/beta live in
+// registers (loaded once per wave, not per row), and the next row is loaded one row ahead.
+template <int NV>  // f16x8 vectors per lane: C ≤ 512·NV
 __global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f16* __restrict__ y, long M, int C,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                    float eps) {
   const int lane = threadIdx.x & 63;
-  const long row = blockIdx.x * 4L + (threadIdx.x >> 6);
-  if (row >= M) return;
   const int CV = C >> 3;
-  const f16* xr = x + row * C;
-  f16x8 v[4];
-  float s = 0.f;
+  float gr[NV][8], br[NV][8];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int cv = lane + 64 * i;
-    if (cv < CV) {
-      v[i] = *(const f16x8*)(xr + cv * 8);
+  for (int i = 0; i < NV; ++i) {
+    const int cv = lane + 64 * i;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += (float)v[i][e];
+    for (int e = 0; e < 8; ++e) {
+      const int c = cv < CV ? cv * 8 + e : 0;
+      gr[i][e] = gamma[c];
+      br[i][e] = beta[c];
     }
   }
-  const float mean = wave_sum(s) / C;
-  float q = 0.f;
+  const long stride = gridDim.x * 4L;
+  long row = blockIdx.x * 4L + (threadIdx.x >> 6);
+  f16x8 vn[NV];
+  auto load = [&](long r) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int cv = lane + 64 * i;
-    if (cv < CV) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float d = (float)v[i][e] - mean;
-        q += d * d;
-      }
+    for (int i = 0; i < NV; ++i) {
+      const int cv = lane + 64 * i;
+      if (r < M && cv < CV) vn[i] = *(const f16x8*)(x + r * C + cv * 8);
     }
-  }
-  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  };
+  load(row);
+  for (; row < M; row += stride) {
+    f16x8 v[NV];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int cv = lane + 64 * i;
-    if (cv < CV) {
-      f16x8 o;
+    for (int i = 0; i < NV; ++i) v[i] = vn[i];
+    load(row + stride);
+    float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        int c = cv * 8 + e;
-        o[e] = (f16)(((float)v[i][e] - mean) * rstd * gamma[c] + beta[c]);
+    for (int i = 0; i < NV; ++i)
+      if (lane + 64 * i < CV)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)v[i][e];
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (lane + 64 * i < CV)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = (float)v[i][e] - mean;
+          q += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int cv = lane + 64 * i;
+      if (cv < CV) {
+        f16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (f16)(((float)v[i][e] - mean) * rstd * gr[i][e] + br[i][e]);
+        *(f16x8*)(y + row * C + cv * 8) = o;
       }
-      *(f16x8*)(y + row * C + cv * 8) = o;
     }
   }
 }
@@ -327,7 +344,17 @@ extern "C" int rdmi_layernorm(const void* x, void* y, long M, int C, const float
                               void* stream) {
   RDMI_REQUIRE(x && y && gamma && beta, RDMI_E_ARG, "layernorm: null pointer");
   RDMI_REQUIRE(C % 8 == 0 && C <= 2048 && M > 0, RDMI_E_ARG, "layernorm: bad C=%d", C);
-  hipLaunchKernelGGL(layernorm_k, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, (const f16*)x,
-                     (f16*)y, M, C, gamma, beta, eps);
+  long blocks = (M + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  const int nv = (C / 8 + 63) / 64;
+  hipStream_t st = (hipStream_t)stream;
+  if (nv == 1)
+    hipLaunchKernelGGL(layernorm_k<1>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+  else if (nv == 2)
+    hipLaunchKernelGGL(layernorm_k<2>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+  else if (nv == 3)
+    hipLaunchKernelGGL(layernorm_k<3>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+  else
+    hipLaunchKernelGGL(layernorm_k<4>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
   return rdmi::check_launch("layernorm");
 }
