@@ -239,7 +239,10 @@ def bench_attn(iters):
 
 def bench_gn(iters):
     for lab, B, HW, C in [("unet 320 96^2 x24", 24, 9216, 320), ("vae 128 768^2 x8", 8, 589824, 128),
-                          ("vae 256 384^2 x8", 8, 147456, 256)]:
+                          ("vae 256 384^2 x8", 8, 147456, 256), ("vae 512 96^2 x15", 15, 9216, 512),
+                          ("vae 512 192^2 x15", 15, 36864, 512), ("unet 320 96^2 x75", 75, 9216, 320),
+                          ("unet 640 48^2 x75", 75, 2304, 640), ("unet 1280 24^2 x75", 75, 576, 1280),
+                          ("unet 1280 12^2 x75", 75, 144, 1280)]:
         x = torch.randn(B, HW, C, device="cuda").half()
         g = torch.ones(C, device="cuda")
         b = torch.zeros(C, device="cuda")
