@@ -78,7 +78,7 @@ def main():
     # snippets per UNet call, a cap (balanced batches, pipeline._snippet_batches): 25 measured
     # 20.9 depth frames/s vs 20.6 at 16 (16/16 had measured +4.5 % over 8/8)
     ap.add_argument("--snippet-batch", type=int, default=25)
-    ap.add_argument("--vae-batch", type=int, default=16)
+    ap.add_argument("--vae-batch", type=int, default=75)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--aligner-iters", type=int, default=2000)
     a = ap.parse_args()

@@ -249,12 +249,18 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     if B > 1 and B * H * W * Cin >= (1 << 30):  # 32-bit buffer offsets: split the batch
         h = B // 2
         rb = rowbias if (rowbias is None or rowbias.dim() == 1) else None
+        # GroupNorm-moment slots of the halves: carved from this call's buffer, or — when this call
+        # is itself one half of a split (_gn_slot) — from the caller's slot range, so that a batch
+        # split twice (≥ 2^31 elements) still writes every image's moments
+        base = (part.data_ptr(), part.stride(0)) if part is not None else _gn_slot
         for s0, s1 in ((0, h), (h, B)):
             slot = None
-            if part is not None and (s0 * Ho * Wo) % 32 == 0:
-                slot = (part.data_ptr() + (s0 * Ho * Wo // 32) * 2 * 4, part.stride(0))
-            elif part is not None:
-                part = None
+            if base is not None and (s0 * Ho * Wo) % 32 == 0:
+                slot = (base[0] + (s0 * Ho * Wo // 32) * 2 * 4, base[1])
+            elif base is not None:
+                if _gn_slot is not None:
+                    raise RuntimeError("conv2d: nested batch split misaligned with the GroupNorm-moment slots")
+                part = base = None
             ig = None
             if in_gn is not None:
                 mr, gamma, beta, groups, silu = in_gn

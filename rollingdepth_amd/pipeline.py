@@ -85,7 +85,7 @@ class RollingDepthPipeline:
         self.text_encoder, self.tokenizer = text_encoder, tokenizer
         self.empty_text_embed: Optional[torch.Tensor] = None
         self.snippet_batch = 25  # max snippets per UNet call (75 frames at snippet length 3)
-        self.vae_batch = 16      # max frames per VAE encode / decode call (capped: _vae_chunks)
+        self.vae_batch = 75      # max frames per VAE encode / decode call (memory-capped: _vae_chunks)
         self._dev = unet.dev
 
     # ------------------------------------------------------------------ construction
@@ -197,13 +197,12 @@ class RollingDepthPipeline:
         return out
 
     def _vae_chunks(self, n: int, h: int, w: int) -> List[Tuple[int, int]]:
-        """Balanced VAE chunks of at most vae_batch frames, capped so that the largest decoder
-        activation (full resolution × 128 channels) stays below 2^31 elements: larger chunks
-        (≥ 29 frames at 768²) were measured to produce NaN latents (an int32 element-count
-        overflow in the VAE path, tools/vae_batch_probe.py), so they are refused here.
-        Also ≤ 32 GB of f32 mid-block attention scores."""
+        """Balanced VAE chunks of at most vae_batch frames, capped so that the mid-block attention's
+        f32 scores ([b, h·w, h·w]) stay ≤ 32 GB and one full-resolution 128-channel activation ≤ 24 GB
+        (768²: 75 frames; 1024²: 30).  Measured at 768² (75-frame snippet batches): 16 → 21.0,
+        38 → 21.1, 75 → 21.2 depth frames/s (profiles/r01_vae_batch_ab.log)."""
         hw = h * w
-        cap = min(self.vae_batch, max(1, int(32e9 // (hw * hw * 4))), max(1, (2 ** 31 - 1) // (hw * 64 * 128)))
+        cap = min(self.vae_batch, max(1, int(32e9 // (hw * hw * 4))), max(1, int(24e9 // (hw * 64 * 128 * 2))))
         return _balanced(n, cap)
 
     def decode_depth(self, z_scaled: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
