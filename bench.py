@@ -1,59 +1,98 @@
 """Benchmark: RollingDepth snippet-denoise hot path on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--res R] [--dilations 1,25]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--preset fast|fast1024|full|paper]
+                    [--frames F | --frames-total T] [--res R] [--dilations 1,25]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver form, one rank per GPU)
 
-Workload (BASELINE.json configs[1], "fast" preset): synthetic 768×768 RGB video of F=100 frames
-per GPU (weak scaling: F·N frames at N GPUs), dilations [1,25] (cap_dilation=True), snippet
-length 3, 1-step DDIM, fp16, no refine; SD2-shaped UNet (866 M) + KL-f8 VAE with random-init
-weights (no checkpoint offline).  One step = RollingDepthPipeline.forward over the whole video
-(encode, every snippet's UNet step + 3 VAE decodes, 2000-iteration DepthAligner, merge,
-renormalise) with frames already resident in HBM.  value = frames processed by all ranks / max
-over ranks of the timed wall time.
+`--gpus N` without a torchrun environment re-launches this script under torch.distributed.run with
+N ranks (before anything touches the GPU) and exits with its status; under torchrun, WORLD_SIZE must
+equal --gpus or the bench exits non-zero.
 
-Extra JSON fields: `roofline` for the dominant kernel (the implicit-GEMM conv/linear kernel or the
-fused attention, whichever has more total time) — achieved = algorithmic FLOPs of every launch of
-that kernel in the timed steps ÷ their summed HIP-event durations (events recorded on the launch
-stream) — and `cpu_baseline`: the CPU oracle (oracle/rd_oracle.py, fp32 PyTorch restatement of
-the reference pipeline, pinned to reference golden vectors) timed on this host on a bounded
-sample: one 3-frame 256² snippet (BASELINE configs[0]).
+Workload (default = BASELINE.json configs[1], the "fast" preset): synthetic 768×768 RGB video,
+dilations [1,25] (cap_dilation=True), snippet length 3, 1-step DDIM, fp16, no refine; SD2-shaped UNet
+(866 M) + KL-f8 VAE with random-init weights (no checkpoint offline).  Weak scaling by default: F=100
+frames per GPU (F·N frames at N GPUs); `--frames-total T` fixes the video length instead (strong
+scaling, e.g. the paper preset's 500 frames).  One step = the whole forward over the video (encode,
+every snippet's UNet step + 3 VAE decodes, 2000-iteration DepthAligner, merge, renormalise, refine
+when the preset has it) with the frames already resident in HBM, outputs copied to pinned host
+memory; at N > 1 shard.sharded_forward (snippet data parallel over RCCL).  value = frames processed
+by all ranks / max over ranks of the timed wall time.
+
+After the timed steps the output is validated (non-zero exit otherwise): depth finite and
+renormalised to [-1, 1], and the first snippet re-run alone (batch 1, its own 3-frame encode) must
+match the batched result within the north_star depth bound (mean |Δ| ≤ 1e-3).
+
+Extra JSON fields: `roofline` for the dominant kernel family by summed time (achieved = algorithmic
+FLOPs of every launch of that family in the timed steps ÷ their summed HIP-event durations, events
+recorded on the launch stream), with the fused attention reported beside it (`roofline.attention`);
+`cpu_baseline`: the CPU oracle (oracle/rd_oracle.py, fp32 PyTorch restatement of the reference
+pipeline, pinned to reference golden vectors) on this host — BASELINE configs[0] (3 frames 256²),
+median of 3 after a warm-up, plus one 3-frame 768² snippet.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 PEAK_F16_TFLOPS = 2500.0  # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3   # MI355X f32-input MFMA (= f32 vector peak)
 PEAK_HBM_GBS = 8000.0
 
+# run_video.py:413-452 presets (BASELINE.json configs[1..4])
+PRESETS = {
+    "fast": dict(res=768, dilations=[1, 25], refine=0, cap=True, dtype="f16", frames=100, frames_total=None),
+    "fast1024": dict(res=1024, dilations=[1, 25], refine=0, cap=True, dtype="f16", frames=100, frames_total=None),
+    "full": dict(res=1024, dilations=[1, 10, 25], refine=10, cap=True, dtype="f16", frames=100, frames_total=None),
+    "paper": dict(res=768, dilations=[1, 10, 25], refine=10, cap=False, dtype="f32", frames=None,
+                  frames_total=500),
+}
 
-def _cpu_baseline():
-    """Oracle forward on a 3-frame 256² snippet (configs[0]), fp32, all host threads."""
+
+def _cpu_threads() -> int:
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    # the pool gives a GPU box a share of its host cores and says so in OMP_NUM_THREADS
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
+def _cpu_baseline(runs_768: int):
+    """Oracle forward (fp32, all granted host threads): configs[0] = one 3-frame 256² snippet,
+    dilation [1], 1 step, 2000-iteration aligner — median of 3 after one warm-up — and one 3-frame
+    768² snippet (`runs_768` runs, median)."""
+    import torch
+
     from oracle import rd_oracle as O
     from rollingdepth_amd import config as C
     from rollingdepth_amd import weights as W
 
-    nthreads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    nthreads = min(nthreads, 16)
+    nthreads = _cpu_threads()
     torch.set_num_threads(nthreads)
     usd = W.synth_state_dict(W.unet_param_shapes(C.SD2_UNET))
     vsd = W.synth_state_dict(W.vae_param_shapes(C.SD2_VAE))
-    frames = W.synth_frames(3, 256, 256, seed=0)
-    noise = W.synth_noise(32, 32)
     ctx = W.synth_context(1024)
-    with torch.no_grad():
-        t0 = time.perf_counter()
-        O.pipeline_forward(usd, C.SD2_UNET, vsd, C.SD2_VAE, C.RD_SCHEDULER, frames, noise, ctx, [1], False)
-        dt = time.perf_counter() - t0
+
+    def run(res):
+        frames = W.synth_frames(3, res, res, seed=0)
+        noise = W.synth_noise(res // 8, res // 8)
+        with torch.no_grad():
+            t0 = time.perf_counter()
+            O.pipeline_forward(usd, C.SD2_UNET, vsd, C.SD2_VAE, C.RD_SCHEDULER, frames, noise, ctx, [1], False)
+            return time.perf_counter() - t0
+
+    run(256)  # warm-up
+    t256 = [run(256) for _ in range(3)]
+    t768 = [run(768) for _ in range(runs_768)]
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -62,9 +101,66 @@ def _cpu_baseline():
                 break
     except OSError:
         pass
-    return {"value": 3.0 / dt, "unit": "depth frames/s", "cores": nthreads, "kind": "port",
-            "sample": f"oracle fp32 RollingDepth forward, 3 frames 256x256, dilation [1], 1 step, "
-                      f"2000-it aligner; {dt:.1f} s on {nthreads} threads ({cpu})"}
+    m256 = statistics.median(t256)
+    out = {"value": round(3.0 / m256, 4), "unit": "depth frames/s", "cores": nthreads, "kind": "port",
+           "sample": f"oracle fp32 RollingDepth forward (CPU restatement pinned to reference goldens), 3 frames "
+                     f"256x256, dilation [1], 1 step, 2000-it aligner: median of 3 after a warm-up "
+                     f"{m256:.2f} s (runs {', '.join(f'{t:.2f}' for t in t256)}) on {nthreads} threads ({cpu})"}
+    if t768:
+        m768 = statistics.median(t768)
+        out["value_768"] = round(3.0 / m768, 5)
+        out["sample_768"] = f"one 3-frame 768x768 snippet, same path: {m768:.1f} s ({len(t768)} run(s))"
+    return out
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _relaunch(n: int) -> int:
+    """Start N ranks under torch.distributed.run as a child (never exec from this process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def _validate(pipe, frames_dev, noise, dil0, snippet0, depth_host, coalign) -> dict:
+    """Output checks after the timed steps; raises on failure."""
+    import torch
+
+    d = depth_host.float()
+    if not torch.isfinite(d).all():
+        raise RuntimeError("bench validation: depth_pred has non-finite values")
+    lo, hi = d.min().item(), d.max().item()
+    if lo < -1.0 - 1e-3 or hi > 1.0 + 1e-3:
+        raise RuntimeError(f"bench validation: depth_pred range [{lo}, {hi}] not within [-1, 1]")
+    info = {"depth_finite": True, "depth_range": [round(lo, 4), round(hi, 4)]}
+    if snippet0 is None:
+        return info
+    # re-run the first snippet of dilation 1 alone: frames 0..2, 1 snippet per UNet call, 3-frame encode
+    lat = pipe.encode_rgb(frames_dev[:3])
+    from rollingdepth_amd import kernels as K
+
+    nz = K.nchw_to_nhwc(noise.to(pipe.device), 8)
+    sb = pipe.snippet_batch
+    pipe.snippet_batch = 1
+    try:
+        again = pipe.init_snippet_infer(lat, nz, [1], [3], [1], [1])[0][0]
+    finally:
+        pipe.snippet_batch = sb
+    a, b = again.float().cpu(), snippet0.float().cpu().reshape(again.shape)
+    if not torch.isfinite(b).all():
+        raise RuntimeError("bench validation: decoded snippets have non-finite values")
+    diff = (a - b).abs()
+    mean, mx, ref = diff.mean().item(), diff.max().item(), b.abs().max().item()
+    info.update(snippet0_rerun_mean_abs=float(f"{mean:.3e}"), snippet0_rerun_max_abs=float(f"{mx:.3e}"))
+    if not (mean <= 1e-3 and mx <= 5e-2 * max(ref, 1e-6)):
+        raise RuntimeError(f"bench validation: batch-1 re-run of snippet 0 differs (mean {mean:.2e}, max {mx:.2e})")
+    return info
 
 
 def main():
@@ -72,20 +168,48 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--frames", type=int, default=100, help="frames per GPU (weak scaling)")
-    ap.add_argument("--res", type=int, default=768)
-    ap.add_argument("--dilations", default="1,25")
+    ap.add_argument("--preset", default="fast", choices=sorted(PRESETS))
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (weak scaling)")
+    ap.add_argument("--frames-total", type=int, default=None, help="total frames (strong scaling)")
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--dilations", default=None)
     # snippets per UNet call, a cap (balanced batches, pipeline._snippet_batches): 25 measured
     # 20.9 depth frames/s vs 20.6 at 16 (16/16 had measured +4.5 % over 8/8)
     ap.add_argument("--snippet-batch", type=int, default=25)
     ap.add_argument("--vae-batch", type=int, default=75)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-768-runs", type=int, default=1)
+    ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--aligner-iters", type=int, default=2000)
     a = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        sys.exit(_relaunch(a.gpus))
+    world = int(world_env or "1")
+    if world != a.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    pr = dict(PRESETS[a.preset])
+    res = a.res or pr["res"]
+    dil0 = [int(x) for x in a.dilations.split(",")] if a.dilations else list(pr["dilations"])
+    if pr["dtype"] != "f16":
+        print(f"bench.py: preset {a.preset} computes in {pr['dtype']}; this build's bench path runs f16 only "
+              f"(a narrower-precision number would not be the reference's arithmetic)", file=sys.stderr)
+        sys.exit(2)
+    if a.frames_total is not None or (a.frames is None and pr["frames_total"] is not None):
+        N = a.frames_total or pr["frames_total"]
+        scaling = "strong"
+    else:
+        N = (a.frames or pr["frames"]) * world
+        scaling = "weak"
+
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -95,28 +219,32 @@ def main():
     from rollingdepth_amd import kernels as K
     from rollingdepth_amd import weights as W
     from rollingdepth_amd.pipeline import RollingDepthPipeline
-    from rollingdepth_amd.shard import sharded_forward
+    from rollingdepth_amd.shard import chunk_bounds, sharded_forward
 
     pipe = RollingDepthPipeline.from_synthetic(C.SD2_UNET, C.SD2_VAE, C.RD_SCHEDULER, device=dev)
     pipe.snippet_batch = a.snippet_batch
     pipe.vae_batch = a.vae_batch
-    N = a.frames * world
-    from rollingdepth_amd.shard import chunk_bounds
     if world > 1:  # each rank materialises only its own chunk of the synthetic video
         lo, hi = chunk_bounds(N, world)[rank]
-        frames = W.synth_frames(N, a.res, a.res, seed=0, first=lo, count=hi - lo).to(dev, torch.float16)
+        frames = W.synth_frames(N, res, res, seed=0, first=lo, count=hi - lo).to(dev, torch.float16)
     else:
-        frames = W.synth_frames(N, a.res, a.res, seed=0)[None].to(dev, torch.float16)
-    noise = W.synth_noise(a.res // 8, a.res // 8).to(dev)
-    dil0 = [int(x) for x in a.dilations.split(",")]
+        frames = W.synth_frames(N, res, res, seed=0)[None].to(dev, torch.float16)
+    noise = W.synth_noise(res // 8, res // 8).to(dev)
     coalign = {"num_iterations": a.aligner_iters}
+    refine = pr["refine"]
+    last = {}
 
     def step():
         if world > 1:
-            return sharded_forward(pipe, frames, list(dil0), True, 3, coalign, init_noise=noise, num_frames=N,
-                                   to_host=True)
-        return pipe.forward(frames, list(dil0), True, [3], [1], [1], coalign, 0, 3, 6, None, False, 4, False,
-                            init_noise=noise)
+            so = sharded_forward(pipe, frames, list(dil0), pr["cap"], 3, coalign, init_noise=noise, num_frames=N,
+                                 to_host=True, refine_step=refine)
+            last["depth"] = so.depth_pred
+            last["snip0"] = so.snippet_rows[0][0] if rank == 0 and so.snippet_rows[0].shape[0] else None
+            return
+        out = pipe.forward(frames, list(dil0), pr["cap"], [3], [1], [1], coalign, refine, 3, 6, None, False, 4,
+                           False, init_noise=noise)
+        last["depth"] = out.depth_pred
+        last["snip0"] = out.snippet_ls[0][0]
 
     for _ in range(a.warmup):
         step()
@@ -137,32 +265,57 @@ def main():
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = tt.item()
+    validation = None
+    if not a.no_validate:
+        try:
+            vframes = frames if world > 1 else frames[0]
+            validation = _validate(pipe, vframes, noise, dil0, last["snip0"] if rank == 0 else None, last["depth"],
+                                   coalign)
+            ok = 1
+        except Exception as e:  # noqa: BLE001 — reported, then non-zero exit
+            print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+            ok = 0
+        if world > 1:
+            t = torch.tensor([ok], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            ok = int(t.item())
+        if not ok:
+            sys.exit(3)
     total_frames = N * a.steps
-    # roofline of the dominant kernel (by summed event time)
-    dom = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
     roof = None
-    if dom:
+    if prof:
+        def _fam(name):
+            p = prof[name]
+            return p["flop"] / (p["ms"] * 1e-3) / 1e12
+
+        dom = max(prof, key=lambda k: prof[k]["ms"])
         p = prof[dom]
-        ach = p["flop"] / (p["ms"] * 1e-3) / 1e12
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": PEAK_F16_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / PEAK_F16_TFLOPS, 4), "traffic": None,
-                "launches": p["n"], "avg_launch_us": round(p["ms"] * 1e3 / max(p["n"], 1), 2),
-                "per_kernel": {k: {"tflops": round(v["flop"] / (v["ms"] * 1e-3) / 1e12, 1),
-                                   "ms": round(v["ms"], 1), "launches": v["n"]} for k, v in prof.items()}}
+        ach = _fam(dom)
+        peak = PEAK_F16_TFLOPS
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": None, "launches": p["n"],
+                "avg_launch_us": round(p["ms"] * 1e3 / max(p["n"], 1), 2),
+                "per_kernel": {k: {"tflops": round(_fam(k), 1), "ms": round(v["ms"], 1), "launches": v["n"]}
+                               for k, v in prof.items()}}
+        if "attention_fwd" in prof:
+            att = _fam("attention_fwd")
+            roof["attention"] = {"achieved": round(att, 1), "peak": peak, "unit": "TFLOP/s",
+                                 "frac": round(att / peak, 4)}
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
-        cpu = _cpu_baseline()
+        cpu = _cpu_baseline(a.cpu_768_runs)
     if rank == 0:
         line = {
             "metric": "depth frames/sec at 768px snip_len=3, 1-step denoise; 1/2/4/8 MI355X",
             "value": round(total_frames / dt, 4), "unit": "depth frames/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 1), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f16", "data": "synthetic",
-            "config": {"workload": f"fast preset: {N}-frame {a.res}x{a.res} video, dilations {dil0} "
-                                   f"(cap_dilation), snippet_len 3, 1-step DDIM, aligner {a.aligner_iters} it, "
-                                   f"no refine; SD2-shaped UNet+VAE random-init",
-                       "frames": N, "res": a.res, "dilations": dil0, "parallelism": f"snippet-dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "scaling": scaling, "vs_baseline": None, "dtype": pr["dtype"], "data": "synthetic",
+            "config": {"workload": f"{a.preset} preset: {N}-frame {res}x{res} video, dilations {dil0} "
+                                   f"(cap_dilation={pr['cap']}), snippet_len 3, 1-step DDIM, aligner "
+                                   f"{a.aligner_iters} it, refine {refine}; SD2-shaped UNet+VAE random-init",
+                       "preset": a.preset, "frames": N, "res": res, "dilations": dil0,
+                       "parallelism": f"snippet-dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "validation": validation,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -28,6 +28,10 @@ extern "C" {
 #define RDMI_E_ALIGN 1002       /* pointer or leading dimension not 16-byte aligned */
 #define RDMI_E_UNSUPPORTED 1003 /* configuration this build does not implement */
 
+/* storage dtype codes of the `dtype` arguments (f32 is the paper preset's arithmetic, run_video.py:444-449) */
+#define RDMI_F16 0
+#define RDMI_F32 1
+
 #define RDMI_EPI_NONE 0
 #define RDMI_EPI_GEGLU 1 /* out[:, n] = (h + b_h) * gelu_erf(g + b_g), weights row-interleaved */
 #define RDMI_EPI_SILU 2  /* out = silu(acc·alpha + bias ...) (TimestepEmbedding act, embeddings.py:543) */
@@ -199,6 +203,15 @@ int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* 
  * (0 ≤ s < n) of src[s][j]; src [n][w][P][ld], out [N][P][ld] f16 (channels ≥ C zeroed). */
 int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld,
                          void* out, void* stream);
+/* Sharded refine averaging (the loop above split over ranks): sum [N][P][C] f32 =
+ * per frame the sum over THIS rank's snippets k0 .. k0+nloc-1 (src [nloc][w][P][ld], dtype RDMI_F16 /
+ * RDMI_F32), zero where none covers the frame; after an all-reduce SUM over ranks,
+ * rdmi_snippet_finish divides by the frame's cover count over all n snippets → out [N][P][ld]
+ * (channels ≥ C zeroed).  World size 1 reproduces rdmi_snippet_average bitwise. */
+int rdmi_snippet_accumulate(const void* src, int dtype, int k0, int nloc, int w, int stride, int N, long P, int C,
+                            int ld, float* sum, void* stream);
+int rdmi_snippet_finish(const float* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
+                        int dtype, void* stream);
 /* Global min/max of an f16 or f32 buffer → minmax[2] f32 (workspace ≥ 2*1024 floats)
  * (the `min([snippet.min() ...])` of depth_aligner.py:78 and the min/max of :316-317). */
 int rdmi_minmax(const void* x, int x_f32, long n, float* minmax, float* workspace, void* stream);
@@ -236,6 +249,18 @@ int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int H, int W, i
 int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                        const float* const* t, const int* n, const int* stride, int w, int seq_len,
                        long HW, const float* shift, float* out, void* stream);
+
+/* Sharded merge: each rank sums s·x+t of ITS full-resolution snippets — rows
+ * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w][HW] — into sum_out [seq_len][HW] f32 (the
+ * same per-slot arithmetic as rdmi_aligner_merge, zero where no local slot covers a frame); after a
+ * reduce-scatter SUM by frame, rdmi_aligner_merge_finish divides frames f0 .. f0+nf-1 by their cover
+ * count over all n[d] snippets.  World size 1 reproduces rdmi_aligner_merge bitwise. */
+int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                               const float* const* t, const int* n, const int* stride, const int* k0,
+                               const int* nloc, int w, int seq_len, long HW, const float* shift, float* sum_out,
+                               void* stream);
+int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w, int f0, int nf, long HW,
+                              const float* sum, float* out, void* stream);
 
 #ifdef __cplusplus
 }

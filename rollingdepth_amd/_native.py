@@ -85,6 +85,8 @@ _SIGS = {
     "rdmi_gather_unet_input": (i32, [vp, i64, vp, i64, i32, vp, i32, i64, vp, vp]),
     "rdmi_ddim_combine": (i32, [vp, i64, vp, i64, vp, i64, i64, i32, i32, f32, f32, f32, i64, vp]),
     "rdmi_snippet_average": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, vp]),
+    "rdmi_snippet_accumulate": (i32, [vp, i32, i32, i32, i32, i32, i32, i64, i32, i32, vp, vp]),
+    "rdmi_snippet_finish": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
     "rdmi_minmax": (i32, [vp, i32, i64, vp, vp, vp]),
     "rdmi_renormalize_f32": (i32, [vp, i64, vp, vp]),
     "rdmi_aligner_workspace": (i64, [C.POINTER(AlignerArgs)]),
@@ -92,7 +94,12 @@ _SIGS = {
     "rdmi_aligner_prepare": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rdmi_aligner_merge": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32),
                                  C.POINTER(i32), i32, i32, i64, vp, vp, vp]),
+    "rdmi_aligner_merge_partial": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32),
+                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64, vp, vp, vp]),
+    "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), i32, i32, i32, i64, vp, vp, vp]),
 }
+
+RDMI_F16, RDMI_F32 = 0, 1
 
 EXPORTED = tuple(_SIGS)
 

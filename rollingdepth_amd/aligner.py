@@ -36,6 +36,26 @@ class DepthAligner:
         return torch.tensor([[i + j * gap for j in range(window_size)]
                              for i in range(sequence_length - (window_size - 1) * gap)])
 
+    @staticmethod
+    def sequence_length(counts: List[int], w: int, dilations: List[int]) -> int:
+        """depth_aligner.py:70-76 (from the first dilation's snippet count)."""
+        return counts[0] + (w - 1) * (dilations[0] - 1) + (w - 1)
+
+    def prepare(self, flat: List[torch.Tensor], shift: torch.Tensor) -> List[torch.Tensor]:
+        """Min shift, border crop, stride subsample (:78-92): [n_d, w, H, W] → f32 [n_d, w, P]."""
+        return [K.aligner_prepare(s, shift, self.border, self.factor) for s in flat]
+
+    def optimize_prepared(self, xs: List[torch.Tensor], strides: List[int], seq_len: int):
+        """The 2000-iteration Adam loop (:123-229) on prepared inputs → (scales [n_d], trans [n_d],
+        history [iters, 3] device tensor, workspace to keep alive until the stream consumed it)."""
+        dev = xs[0].device
+        scales = [torch.ones(x.shape[0], dtype=torch.float32, device=dev) for x in xs]
+        trans = [torch.zeros(x.shape[0], dtype=torch.float32, device=dev) for x in xs]
+        hist = torch.zeros((max(self.num_iterations, 1), 3), dtype=torch.float32, device=dev)
+        ws = K.aligner_optimize(xs, scales, trans, strides, seq_len, self.lr, (0.5, 0.9), 1e-8, self.lmda2,
+                                self.lmda3, self.depth_loss_weight, self.loss_scale, self.num_iterations, hist)
+        return scales, trans, hist, ws
+
     def run(self, snippet_ls: List[torch.Tensor], dilations: List[int]):
         dev = torch.device(self.device)
         snippet_ls = [s.to(dev) for s in snippet_ls]
@@ -44,7 +64,7 @@ class DepthAligner:
             raise NotImplementedError("DepthAligner (librdmi): all dilations must share one snippet length")
         w = lengths[0]
         gaps = [d - 1 for d in dilations]
-        seq_len = len(snippet_ls[0]) + (w - 1) * gaps[0] + (w - 1)
+        seq_len = self.sequence_length([s.shape[0] for s in snippet_ls], w, dilations)
         for s, g in zip(snippet_ls, gaps):
             expect = seq_len - (w - 1) * (g + 1)
             if s.shape[0] != expect:
@@ -54,13 +74,9 @@ class DepthAligner:
         # global min over every snippet (depth_aligner.py:78)
         mins = torch.stack([K.minmax(s) for s in flat]).reshape(-1)
         shift = K.minmax(mins)
-        xs = [K.aligner_prepare(s, shift, self.border, self.factor) for s in flat]
-        scales = [torch.ones(x.shape[0], dtype=torch.float32, device=dev) for x in xs]
-        trans = [torch.zeros(x.shape[0], dtype=torch.float32, device=dev) for x in xs]
-        hist = torch.zeros((max(self.num_iterations, 1), 3), dtype=torch.float32, device=dev)
+        xs = self.prepare(flat, shift)
         strides = [g + 1 for g in gaps]
-        ws = K.aligner_optimize(xs, scales, trans, strides, seq_len, self.lr, (0.5, 0.9), 1e-8, self.lmda2,
-                                self.lmda3, self.depth_loss_weight, self.loss_scale, self.num_iterations, hist)
+        scales, trans, hist, ws = self.optimize_prepared(xs, strides, seq_len)
         merged = K.aligner_merge(flat, scales, trans, strides, seq_len, shift)
         merged = merged.to(dtype)[:, None]
         loss_ls = [tuple(r) for r in hist[: self.num_iterations].tolist()]

@@ -260,14 +260,29 @@ struct MergeP {
   const float* s[MAXD];
   const float* t[MAXD];
   int n[MAXD], stride[MAXD];
+  int k0[MAXD], nloc[MAXD];  // rows of x[d] are global snippets k0[d] .. k0[d]+nloc[d]-1
   int nd, w, xf32;
+  int sum_only;              // 1: write the per-frame sum (sharded merge), 0: the mean
+  int f0;                    // first frame of out (out rows are frames f0 .. f0+gridDim.y-1)
   long HW;
   const float* shift;
   float* out;
 };
 
+// number of (dilation, slot) pairs covering frame f (the B.sum(0) of depth_aligner.py:190 / the
+// length of the torch.cat of :258)
+__device__ __forceinline__ int cover_count(const int* n, const int* stride, int nd, int w, int f) {
+  int cnt = 0;
+  for (int d = 0; d < nd; ++d)
+    for (int j = 0; j < w; ++j) {
+      const int k = f - j * stride[d];
+      cnt += (k >= 0 && k < n[d]) ? 1 : 0;
+    }
+  return cnt;
+}
+
 __global__ void merge_k(MergeP p) {
-  const int f = blockIdx.y;
+  const int f = p.f0 + blockIdx.y;
   const float sh = p.shift ? p.shift[0] : 0.f;
   for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
     float sum = 0.f;
@@ -275,8 +290,8 @@ __global__ void merge_k(MergeP p) {
     for (int d = 0; d < p.nd; ++d) {
       for (int j = p.w - 1; j >= 0; --j) {  // boolean-mask order over [n_d, w]: k ascending
         int k = f - j * p.stride[d];
-        if (k < 0 || k >= p.n[d]) continue;
-        long off = ((long)k * p.w + j) * p.HW + px;
+        if (k < p.k0[d] || k >= p.k0[d] + p.nloc[d]) continue;
+        long off = ((long)(k - p.k0[d]) * p.w + j) * p.HW + px;
         float a;
         if (p.xf32) {
           float xs = ((const float*)p.x[d])[off] - sh;
@@ -291,7 +306,18 @@ __global__ void merge_k(MergeP p) {
         ++cnt;
       }
     }
-    p.out[(long)f * p.HW + px] = cnt ? sum / (float)cnt : 0.f;
+    p.out[(long)blockIdx.y * p.HW + px] = p.sum_only ? sum : (cnt ? sum / (float)cnt : 0.f);
+  }
+}
+
+// sharded merge, second half: out[f] = sum[f] / (number of covering slots of frame f0 + f over ALL
+// snippets), after the per-rank sums were reduced over ranks
+__global__ void merge_finish_k(MergeP p, const float* __restrict__ sum) {
+  const int fl = blockIdx.y;
+  const int cnt = cover_count(p.n, p.stride, p.nd, p.w, p.f0 + fl);
+  for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
+    const long i = (long)fl * p.HW + px;
+    p.out[i] = cnt ? sum[i] / (float)cnt : 0.f;
   }
 }
 
@@ -397,21 +423,60 @@ extern "C" int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int 
   return rdmi::check_launch("aligner_prepare");
 }
 
-extern "C" int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
-                                  const float* const* t, const int* n, const int* stride, int w, int seq_len, long HW,
-                                  const float* shift, float* out, void* stream) {
-  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && out && HW > 0, RDMI_E_ARG, "aligner_merge: bad args");
+static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float* const* s, const float* const* t,
+                        const int* n, const int* stride, const int* k0, const int* nloc, int w, int f0, int nf,
+                        long HW, const float* shift, float* out, int sum_only, void* stream) {
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && out && HW > 0 && nf >= 0 && f0 >= 0, RDMI_E_ARG,
+               "aligner_merge: bad args");
   MergeP p{};
   for (int d = 0; d < n_dil; ++d) {
+    const int kk = k0 ? k0[d] : 0, nl = nloc ? nloc[d] : n[d];
+    RDMI_REQUIRE(kk >= 0 && nl >= 0 && kk + nl <= n[d] && (nl == 0 || (xf[d] && s[d] && t[d])), RDMI_E_ARG,
+                 "aligner_merge: dilation %d rows %d+%d of %d", d, kk, nl, n[d]);
     p.x[d] = xf[d];
     p.s[d] = s[d];
     p.t[d] = t[d];
     p.n[d] = n[d];
     p.stride[d] = stride[d];
+    p.k0[d] = kk;
+    p.nloc[d] = nl;
   }
   p.nd = n_dil; p.w = w; p.xf32 = x_f32; p.HW = HW; p.shift = shift; p.out = out;
+  p.sum_only = sum_only; p.f0 = f0;
+  if (nf == 0) return 0;
   long gx = (HW + 255) / 256;
   if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(merge_k, dim3((unsigned)gx, seq_len), dim3(256), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(merge_k, dim3((unsigned)gx, nf), dim3(256), 0, (hipStream_t)stream, p);
   return rdmi::check_launch("aligner_merge");
+}
+
+extern "C" int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                                  const float* const* t, const int* n, const int* stride, int w, int seq_len, long HW,
+                                  const float* shift, float* out, void* stream) {
+  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, nullptr, nullptr, w, 0, seq_len, HW, shift, out, 0, stream);
+}
+
+extern "C" int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                                          const float* const* t, const int* n, const int* stride, const int* k0,
+                                          const int* nloc, int w, int seq_len, long HW, const float* shift,
+                                          float* sum_out, void* stream) {
+  RDMI_REQUIRE(k0 && nloc, RDMI_E_ARG, "aligner_merge_partial: k0/nloc required");
+  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, 0, seq_len, HW, shift, sum_out, 1, stream);
+}
+
+extern "C" int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w, int f0, int nf, long HW,
+                                         const float* sum, float* out, void* stream) {
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && sum && out && HW > 0 && f0 >= 0 && nf >= 0, RDMI_E_ARG,
+               "aligner_merge_finish: bad args");
+  if (nf == 0) return 0;
+  MergeP p{};
+  for (int d = 0; d < n_dil; ++d) {
+    p.n[d] = n[d];
+    p.stride[d] = stride[d];
+  }
+  p.nd = n_dil; p.w = w; p.HW = HW; p.out = out; p.f0 = f0;
+  long gx = (HW + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(merge_finish_k, dim3((unsigned)gx, nf), dim3(256), 0, (hipStream_t)stream, p, sum);
+  return rdmi::check_launch("aligner_merge_finish");
 }

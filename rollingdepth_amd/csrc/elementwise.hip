@@ -143,6 +143,46 @@ __global__ void snippet_average_k(const f16* __restrict__ src, int n, int w, int
   }
 }
 
+// sharded refine (rollingdepth_pipeline.py:586-629 split over ranks): the per-frame f32 sum over
+// this rank's snippets k0 .. k0+nloc-1 (snippet index ascending, as snippet_average_k), for all N
+// frames (zeros where no local snippet covers f) — all-reduced over ranks, then snippet_finish_k
+template <typename T>
+__global__ void snippet_accumulate_k(const T* __restrict__ src, int k0, int nloc, int w, int stride, long P, int C,
+                                     int ld, float* __restrict__ sum) {
+  const int f = blockIdx.y;
+  const long tot = P * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / C;
+    const int c = (int)(i - p * C);
+    float s = 0.f;
+    for (int j = w - 1; j >= 0; --j) {
+      const int sn = f - j * stride;
+      if (sn < k0 || sn >= k0 + nloc) continue;
+      s += (float)src[((long)(sn - k0) * w + j) * P * ld + p * ld + c];
+    }
+    sum[(long)f * tot + i] = s;
+  }
+}
+
+template <typename T>
+__global__ void snippet_finish_k(const float* __restrict__ sum, int n, int w, int stride, long P, int C, int ld,
+                                 T* __restrict__ out) {
+  const int f = blockIdx.y;
+  int cnt = 0;
+  for (int j = 0; j < w; ++j) {
+    const int sn = f - j * stride;
+    cnt += (sn >= 0 && sn < n) ? 1 : 0;
+  }
+  const long tot = P * ld;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const long p = i / ld;
+    const int c = (int)(i - p * ld);
+    float v = 0.f;
+    if (c < C && cnt) v = sum[((long)f * P + p) * C + c] / (float)cnt;
+    out[(long)f * tot + i] = (T)v;
+  }
+}
+
 // 16-B vector loads (8 halves / 4 floats per lane and step), scalar tail; min/max are
 // order-independent, so the result is exact whatever the split.
 __global__ __launch_bounds__(256) void minmax_partial(const void* __restrict__ x, int xf32, long n,
@@ -302,4 +342,33 @@ extern "C" int rdmi_snippet_average(const void* src, int n, int w, int stride, i
   hipLaunchKernelGGL(snippet_average_k, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream, (const f16*)src, n, w,
                      stride, P, C, ld, (f16*)out);
   return rdmi::check_launch("snippet_average");
+}
+
+extern "C" int rdmi_snippet_accumulate(const void* src, int dtype, int k0, int nloc, int w, int stride, int N, long P,
+                                       int C, int ld, float* sum, void* stream) {
+  RDMI_REQUIRE(sum && N > 0 && w > 0 && ld >= C && k0 >= 0 && nloc >= 0 && (nloc == 0 || src), RDMI_E_ARG,
+               "snippet_accumulate: bad args");
+  long gx = (P * C + 255) / 256;
+  if (gx > 4096) gx = 4096;
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(snippet_accumulate_k<float>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)src, k0, nloc, w, stride, P, C, ld, sum);
+  else
+    hipLaunchKernelGGL(snippet_accumulate_k<f16>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream,
+                       (const f16*)src, k0, nloc, w, stride, P, C, ld, sum);
+  return rdmi::check_launch("snippet_accumulate");
+}
+
+extern "C" int rdmi_snippet_finish(const float* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
+                                   int dtype, void* stream) {
+  RDMI_REQUIRE(sum && out && n > 0 && w > 0 && N > 0 && ld >= C, RDMI_E_ARG, "snippet_finish: bad args");
+  long gx = (P * ld + 255) / 256;
+  if (gx > 4096) gx = 4096;
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(snippet_finish_k<float>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream, sum, n, w,
+                       stride, P, C, ld, (float*)out);
+  else
+    hipLaunchKernelGGL(snippet_finish_k<f16>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream, sum, n, w,
+                       stride, P, C, ld, (f16*)out);
+  return rdmi::check_launch("snippet_finish");
 }

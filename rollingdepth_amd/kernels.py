@@ -246,6 +246,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     if out is None:
         out = torch.empty((B, Ho, Wo, cout), dtype=F16, device=x.device)
     part = _gn_part(out, B * Ho * Wo, cout) if gn and _gn_slot is None else None
+    if part is not None and not _split_slots_aligned(B, H * W * Cin, Ho * Wo):
+        part = None  # some split level misaligns the moment slots: the next groupnorm computes them
     if B > 1 and B * H * W * Cin >= (1 << 30):  # 32-bit buffer offsets: split the batch
         h = B // 2
         rb = rowbias if (rowbias is None or rowbias.dim() == 1) else None
@@ -255,12 +257,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
         base = (part.data_ptr(), part.stride(0)) if part is not None else _gn_slot
         for s0, s1 in ((0, h), (h, B)):
             slot = None
-            if base is not None and (s0 * Ho * Wo) % 32 == 0:
+            if base is not None:  # alignment of every level was checked at the top (_split_slots_aligned)
                 slot = (base[0] + (s0 * Ho * Wo // 32) * 2 * 4, base[1])
-            elif base is not None:
-                if _gn_slot is not None:
-                    raise RuntimeError("conv2d: nested batch split misaligned with the GroupNorm-moment slots")
-                part = base = None
             ig = None
             if in_gn is not None:
                 mr, gamma, beta, groups, silu = in_gn
@@ -284,6 +282,16 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     if _gn_slot is None:
         _gn_attach(out, part)
     return out
+
+
+def _split_slots_aligned(B: int, elems_per_image: int, howo: int) -> bool:
+    """Whether every level of conv2d's recursive batch split (B > 1 and ≥ 2^30 input elements)
+    starts its second half on a 32-row GroupNorm-moment slot boundary."""
+    if B <= 1 or B * elems_per_image < (1 << 30):
+        return True
+    h = B // 2
+    return (h * howo) % 32 == 0 and _split_slots_aligned(h, elems_per_image, howo) and \
+        _split_slots_aligned(B - h, elems_per_image, howo)
 
 
 def conv2d_in_gn_supported(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, groups: int, stride: int = 1,
@@ -578,6 +586,37 @@ def snippet_average(src: torch.Tensor, stride: int, N: int, c: int = 4) -> torch
     return out
 
 
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == F16:
+        return _N.RDMI_F16
+    if t.dtype == F32:
+        return _N.RDMI_F32
+    raise TypeError(f"expected f16 or f32, got {t.dtype}")
+
+
+def snippet_accumulate(src: torch.Tensor, k0: int, stride: int, N: int, c: int = 4,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sharded refine, rank-local half: src [nloc, w, h, wd, ld] (global snippets k0 .. k0+nloc-1) →
+    f32 [N, h·wd, c] per-frame sums over the local snippets (zeros elsewhere)."""
+    nloc, w, h, wd, ld = src.shape
+    src = src.contiguous()
+    out = torch.empty((N, h * wd, c), dtype=F32, device=src.device) if out is None else out
+    check(lib.rdmi_snippet_accumulate(src.data_ptr() if nloc else None, _dtype_code(src), k0, nloc, w, stride, N,
+                                      h * wd, c, ld, out.data_ptr(), _stream()), "rdmi_snippet_accumulate")
+    return out
+
+
+def snippet_finish(sums: torch.Tensor, n: int, w: int, stride: int, hw, ld: int, dtype=F16) -> torch.Tensor:
+    """Sharded refine, after the all-reduce: f32 [N, P, c] sums → [N, h, wd, ld] means (÷ the frame's
+    cover count over all n snippets)."""
+    N, P, c = sums.shape
+    h, wd = hw
+    out = torch.empty((N, h, wd, ld), dtype=dtype, device=sums.device)
+    check(lib.rdmi_snippet_finish(sums.data_ptr(), n, w, stride, N, P, c, ld, out.data_ptr(), _dtype_code(out),
+                                  _stream()), "rdmi_snippet_finish")
+    return out
+
+
 def minmax(x: torch.Tensor) -> torch.Tensor:
     if x.dtype not in (F16, F32):
         raise TypeError("minmax: f16/f32 expected")
@@ -644,4 +683,35 @@ def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: i
     stv = (C.c_int * nd)(*list(strides))
     check(lib.rdmi_aligner_merge(nd, xp, int(xf[0].dtype == F32), sp, tp, nn, stv, w, seq_len, H * W,
                                  shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge")
+    return out
+
+
+def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int], n: Sequence[int], scales, trans,
+                          strides, w: int, seq_len: int, HW: int, shift: torch.Tensor, x_f32: bool,
+                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sharded merge, rank-local half: xf[d] [nloc_d, w, H, W] = global snippets k0[d] .. of dilation
+    d (None / 0 rows when the rank owns none) → f32 [seq_len, HW] per-frame sums of s·x+t."""
+    nd = len(xf)
+    out = torch.empty((seq_len, HW), dtype=F32, device=shift.device) if out is None else out
+    xp = (C.c_void_p * nd)(*[(x.data_ptr() if x is not None and x.shape[0] else None) for x in xf])
+    sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
+    tp = (C.c_void_p * nd)(*[t.data_ptr() for t in trans])
+    nn = (C.c_int * nd)(*list(n))
+    kk = (C.c_int * nd)(*list(k0))
+    nl = (C.c_int * nd)(*[(x.shape[0] if x is not None else 0) for x in xf])
+    stv = (C.c_int * nd)(*list(strides))
+    check(lib.rdmi_aligner_merge_partial(nd, xp, int(x_f32), sp, tp, nn, stv, kk, nl, w, seq_len, HW,
+                                         shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge_partial")
+    return out
+
+
+def aligner_merge_finish(sums: torch.Tensor, n: Sequence[int], strides: Sequence[int], w: int, f0: int) -> torch.Tensor:
+    """Sharded merge, after the reduce-scatter: f32 [nf, HW] sums of frames f0 .. → per-frame means."""
+    nf, HW = sums.shape
+    nd = len(n)
+    out = torch.empty_like(sums)
+    nn = (C.c_int * nd)(*list(n))
+    stv = (C.c_int * nd)(*list(strides))
+    check(lib.rdmi_aligner_merge_finish(nd, nn, stv, w, f0, nf, HW, sums.data_ptr(), out.data_ptr(), _stream()),
+          "rdmi_aligner_merge_finish")
     return out

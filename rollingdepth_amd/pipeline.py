@@ -39,10 +39,21 @@ F16, F32 = torch.float16, torch.float32
 
 @dataclass
 class RollingDepthOutput:
+    """rollingdepth_pipeline.py RollingDepthOutput (input_rgb, depth_pred, snippet_ls, depth_coaligned).
+
+    The fork's CLI (run_video.py:587-606) was written against the IC-Light experiment's output
+    (rollingimg_pipeline.py:424-433) and reads R_pred / G_pred / B_pred / aligned_snippet_pred_ls;
+    for the depth pipeline those are filled (by __call__ only) as a compatibility decision
+    (SURVEY.md §8b): R = G = B = depth·0.5 + 0.5 ([N,1,H,W] in [0,1], what run_video multiplies by
+    255) and aligned_snippet_pred_ls = [the co-aligned depth repeated to 3 channels]."""
     input_rgb: torch.Tensor
     depth_pred: torch.Tensor
     snippet_ls: Optional[List[torch.Tensor]]
     depth_coaligned: Optional[torch.Tensor]
+    R_pred: Optional[torch.Tensor] = None
+    G_pred: Optional[torch.Tensor] = None
+    B_pred: Optional[torch.Tensor] = None
+    aligned_snippet_pred_ls: Optional[List[torch.Tensor]] = None
 
     def __getitem__(self, k):
         return getattr(self, k)
@@ -75,6 +86,12 @@ def _balanced(n: int, cap: int) -> List[Tuple[int, int]]:
     return out
 
 
+def _contiguous_range(total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Rank's share of `total` equal-cost units: W contiguous ranges of ceil(total/W)."""
+    c = (total + world - 1) // world
+    return min(rank * c, total), min((rank + 1) * c, total)
+
+
 class RollingDepthPipeline:
     rgb_latent_scale_factor = 0.18215
     depth_latent_scale_factor = 0.18215
@@ -87,6 +104,7 @@ class RollingDepthPipeline:
         self.snippet_batch = 25  # max snippets per UNet call (75 frames at snippet length 3)
         self.vae_batch = 75      # max frames per VAE encode / decode call (memory-capped: _vae_chunks)
         self._dev = unet.dev
+        self._group = None  # torch.distributed group for snippet-parallel forward (enable_snippet_parallel)
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -125,10 +143,39 @@ class RollingDepthPipeline:
     def dtype(self):
         return F16
 
-    def to(self, device):
-        if torch.device(device) != self._dev:
-            raise NotImplementedError("construct the pipeline on its target device")
+    def to(self, *args, **kwargs):
+        """DiffusionPipeline.to (pipeline_utils.py:303): weights already live on the device the
+        pipeline was built for.  Accepts that device (an index-less "cuda" names the current device),
+        a dtype equal to the pipeline's, or both; anything else raises."""
+        for a in list(args) + list(kwargs.values()):
+            if a is None:
+                continue
+            if isinstance(a, torch.dtype):
+                if a != self.dtype:
+                    raise NotImplementedError(f"pipeline built for {self.dtype}; rebuild it with torch_dtype={a}")
+                continue
+            d = torch.device(a)
+            idx = d.index if d.index is not None else (torch.cuda.current_device() if d.type == "cuda" else None)
+            if d.type != self._dev.type or idx != self._dev.index:
+                raise NotImplementedError(f"pipeline lives on {self._dev}; construct it on {d} instead")
         return self
+
+    def enable_snippet_parallel(self, group=None):
+        """Run forward() snippet-parallel over the ranks of `group` (default: the world group; one
+        process per GPU, torch.distributed initialised with backend "nccl" = RCCL).  Every rank calls
+        forward() with the same arguments and receives the full outputs (shard.py holds the plan)."""
+        import torch.distributed as dist
+        self._group = group if group is not None else dist.group.WORLD
+        return self
+
+    def enable_xformers_memory_efficient_attention(self, attention_op=None):
+        """pipeline_utils.py:1630.  The cross-frame attention of every UNet / VAE Attention already runs
+        on librdmi's fused flash kernel (memory-efficient by construction), so this only records the
+        request; run_video.py:534-538 calls it unconditionally."""
+        self._xformers_requested = True
+
+    def disable_xformers_memory_efficient_attention(self):
+        self._xformers_requested = False
 
     def encode_empty_text(self):
         """rollingdepth_pipeline.py:178-191 — needs the CLIP text encoder; the build caches the
@@ -184,6 +231,14 @@ class RollingDepthPipeline:
             h.copy_(t, non_blocking=True)
         t.record_stream(stream)
         return h
+
+    def _noise_nhwc(self, init_noise: torch.Tensor, h: int, w: int) -> torch.Tensor:
+        """[1, 4, h, w] (or [4, h, w]) init noise → NHWC [1, h, w, 8] on the device; the shape is checked
+        because the UNet-input gather broadcasts h·w pixels out of it."""
+        n = init_noise if init_noise.dim() == 4 else init_noise[None]
+        if tuple(n.shape) != (1, self.N_CHANNEL_PER_LATENT, h, w):
+            raise ValueError(f"init_noise shape {tuple(init_noise.shape)} != (1, 4, {h}, {w}) (the latent size)")
+        return K.nchw_to_nhwc(n.to(self.device), 8)
 
     # ------------------------------------------------------------------ stages
     def encode_rgb(self, frames_nchw: torch.Tensor) -> torch.Tensor:
@@ -245,10 +300,10 @@ class RollingDepthPipeline:
             self.scheduler.set_timesteps(steps)
             timesteps = self.scheduler.timesteps
             idx = self.get_snippet_indice(0, timesteps, N, slen, dil, dil, stride)
-            buf = torch.empty((len(idx), slen, H, W), dtype=F16, device=self.device)
             todo = list(range(len(idx))) if snippet_subset is None else list(snippet_subset[di])
+            # row r of the output is snippet todo[r] (all snippets unless a subset is given)
+            buf = torch.empty((len(todo), slen, H, W), dtype=F16, device=self.device)
             fidx_all = self._device_index([f for s in todo for f in idx[s]]) if todo else None
-            pos_all = self._device_index(todo) if todo else None
             for b0, b1 in self._snippet_batches(len(todo), slen, h, w):
                 sel = todo[b0:b1]
                 fidx = fidx_all[b0 * slen:(b0 + len(sel)) * slen]
@@ -273,19 +328,25 @@ class RollingDepthPipeline:
                         self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4, out=x2[..., 4:])
                         x = x2
                         depth_view = x[..., 4:8]
-                dec = buf[sel[0]:sel[-1] + 1] if sel == list(range(sel[0], sel[-1] + 1)) else None
-                tgt = torch.empty((len(sel) * slen, H, W, 1), dtype=F16, device=self.device) if dec is None \
-                    else dec.view(len(sel) * slen, H, W, 1)
-                self.decode_depth(zin, tgt)
-                if dec is None:
-                    buf[pos_all[b0:b0 + len(sel)].long()] = tgt.view(len(sel), slen, H, W)
+                self.decode_depth(zin, buf[b0:b1].view(len(sel) * slen, H, W, 1))
             outs.append(buf)
         return outs
 
     def refine(self, rgb_latent: torch.Tensor, depth_latents: torch.Tensor, init_noise: torch.Tensor,
-               refine_step: int, snippet_len: int, start_dilation: int, skip_t_ratio: float = 0.5) -> torch.Tensor:
+               refine_step: int, snippet_len: int, start_dilation: int, skip_t_ratio: float = 0.5,
+               group=None) -> torch.Tensor:
         """rollingdepth_pipeline.py:517-633 on device.  rgb_latent / depth_latents NHWC [N,h,w,8]
-        (channels 0..3), init_noise NHWC [1,h,w,8].  Returns the refined latents [N,h,w,8]."""
+        (channels 0..3), init_noise NHWC [1,h,w,8].  Returns the refined latents [N,h,w,8].
+
+        `group` (a torch.distributed process group of W > 1 ranks): every rank
+        holds all N latents; each step's snippet list is split into W contiguous ranges, each rank runs
+        the UNet on its range and sums its predictions per frame, and one all-reduce SUM of the
+        [N, h·w, 4] f32 sums (+ the cover count, which is data-independent) gives every rank the
+        step's averaged latents."""
+        world, rank = 1, 0
+        if group is not None:
+            import torch.distributed as dist
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
         self._context()
         N, h, w, _ = rgb_latent.shape
         T = int(refine_step / skip_t_ratio)
@@ -300,18 +361,26 @@ class RollingDepthPipeline:
         for i_step, t in enumerate(ts):
             idx = self.get_snippet_indice(i_step, ts, N, snippet_len, start_dilation, 1, 1)
             stride = idx[0][1] - idx[0][0] if snippet_len > 1 else 1
-            preds = torch.empty((len(idx), snippet_len, h, w, 8), dtype=F16, device=self.device)
-            fidx_all = self._device_index([f for s in idx for f in s])
-            for b0, b1 in self._snippet_batches(len(idx), snippet_len, h, w):
-                sel = idx[b0:b1]
+            covered = {f for s in idx for f in s}
+            assert len(covered) == N, "refine: every frame must be covered by a snippet"
+            lo, hi = _contiguous_range(len(idx), world, rank)
+            mine = idx[lo:hi]
+            preds = torch.empty((len(mine), snippet_len, h, w, 8), dtype=F16, device=self.device)
+            fidx_all = self._device_index([f for s in mine for f in s]) if mine else None
+            for b0, b1 in self._snippet_batches(len(mine), snippet_len, h, w):
+                sel = mine[b0:b1]
                 fidx = fidx_all[b0 * snippet_len:(b0 + len(sel)) * snippet_len]
                 x = K.gather_unet_input(rgb_latent, new, fidx, depth_bcast=False)
                 pred = self.unet.forward(x, int(t), num_view=snippet_len)
                 self.scheduler.step_(pred, int(t), x[..., 4:8], 1.0, channels=4,
                                      out=preds[b0:b0 + len(sel)].view(len(sel) * snippet_len, h, w, 8))
-            covered = {f for s in idx for f in s}
-            assert len(covered) == N, "refine: every frame must be covered by a snippet"
-            new = K.snippet_average(preds, stride, N)
+            if world == 1:
+                new = K.snippet_average(preds, stride, N)
+            else:
+                import torch.distributed as dist
+                sums = K.snippet_accumulate(preds, lo, stride, N)
+                dist.all_reduce(sums, group=group)
+                new = K.snippet_finish(sums, len(idx), snippet_len, stride, (h, w), 8)
         return new
 
     # ------------------------------------------------------------------ entry points
@@ -333,9 +402,40 @@ class RollingDepthPipeline:
             frames, _ = load_video_frames(src, start_frame, frame_count, processing_res, resample_method, verbose)
         if restore_res:
             raise NotImplementedError("restore_res needs torchvision resize (absent from this image)")
-        return self.forward(frames[None] if frames.dim() == 4 else frames, dilations, cap_dilation, snippet_lengths,
-                            init_infer_steps, strides, coalign_kwargs, refine_step, refine_snippet_len,
-                            refine_start_dilation, generator, verbose, max_vae_bs, unload_snippet, **kw)
+        kw.pop("input_bg_video_path", None)  # fork CLI (run_video.py:563): IC-Light background, unused here
+        out = self.forward(frames[None] if frames.dim() == 4 else frames, dilations, cap_dilation, snippet_lengths,
+                           init_infer_steps, strides, coalign_kwargs, refine_step, refine_snippet_len,
+                           refine_start_dilation, generator, verbose, max_vae_bs, unload_snippet, **kw)
+        if input_fg_video_path is not None:
+            rgb = out.depth_pred.float() * 0.5 + 0.5
+            out.R_pred = out.G_pred = out.B_pred = rgb
+            out.aligned_snippet_pred_ls = [out.depth_coaligned.float().expand(-1, 3, -1, -1)]
+        return out
+
+    def _forward_sharded(self, input_frames, dilations, snippet_lengths, coalign_kwargs, refine_step,
+                         refine_snippet_len, refine_start_dilation, init_noise, record):
+        """forward() over W ranks (shard.sharded_forward), outputs assembled on every rank.  Dilations
+        arrive already capped (forward's checks ran); the snippets are all-gathered at full
+        resolution only here, to honour the snippet_ls contract (bench.py keeps them distributed)."""
+        import torch.distributed as dist
+        from .shard import gather_rows_by_dilation, sharded_forward
+
+        if len(set(snippet_lengths)) != 1:
+            raise NotImplementedError("snippet-parallel forward: one snippet length for all dilations")
+        world = dist.get_world_size(self._group)
+        so = sharded_forward(self, input_frames, list(dilations), False, snippet_lengths[0], coalign_kwargs,
+                             init_noise=init_noise, group=self._group, refine_step=refine_step,
+                             refine_snippet_len=refine_snippet_len, refine_start_dilation=refine_start_dilation,
+                             gather=True, record=record)
+        snips = gather_rows_by_dilation(so.snippet_rows, so.snippet_counts, world, self._group)
+        H, W = so.depth_pred_full.shape[-2:]
+        d2h = torch.cuda.Stream(self.device)
+        snip_host = [self._to_host_async(s.view(s.shape[0], s.shape[1], 1, H, W), d2h) for s in snips]
+        rgb = input_frames[0].to(self.device, F16) / 2.0 + 0.5
+        outs = [self._to_host_async(t, d2h) for t in (rgb, so.depth_pred_full, so.depth_coaligned_full)]
+        d2h.synchronize()
+        return RollingDepthOutput(input_rgb=outs[0], depth_pred=outs[1], snippet_ls=snip_host,
+                                  depth_coaligned=outs[2])
 
     @torch.no_grad()
     def forward(self, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool,
@@ -369,6 +469,11 @@ class RollingDepthPipeline:
             refine_start_dilation = self.cap_max_dilation(seq_len, refine_snippet_len, refine_start_dilation, verbose)
         if input_frames.shape[0] != 1:
             raise NotImplementedError("Layered inference is only implemented for B=1")
+        if self._group is not None:
+            import torch.distributed as dist
+            if dist.get_world_size(self._group) > 1:
+                return self._forward_sharded(input_frames, dilations, snippet_lengths, coalign_kwargs, refine_step,
+                                             refine_snippet_len, refine_start_dilation, init_noise, record)
         # ----------------- encode (H2D boundary :263)
         frames = input_frames[0].to(self.device)
         rgb_latent = self.encode_rgb(frames)
@@ -376,7 +481,7 @@ class RollingDepthPipeline:
         # ----------------- shared init noise (:282-288)
         if init_noise is None:
             init_noise = torch.randn((1, 4, h, w), device=self.device, dtype=F16, generator=generator)
-        noise = K.nchw_to_nhwc(init_noise.to(self.device), 8)
+        noise = self._noise_nhwc(init_noise, h, w)
         snippets = self.init_snippet_infer(rgb_latent, noise, dilations, snippet_lengths, init_infer_steps, strides,
                                            record=record)
         # snippet_ls D2H (the reference returns it on the host) overlaps the aligner's kernels

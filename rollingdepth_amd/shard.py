@@ -1,24 +1,42 @@
 """Snippet data-parallel sharding across the GPUs of one node.
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI):
-  1. frames are split into W equal contiguous chunks; each rank VAE-encodes its chunk and the
-     latents are all-gathered (73.7 KB/frame at 768², negligible on xGMI);
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Per forward:
+  1. frames are split into W contiguous chunks; each rank VAE-encodes its chunk and the latents are
+     all-gathered ([N, h, w, 8] f16, 147 KB/frame at 768²);
   2. the flattened (dilation, snippet) list of rollingdepth_pipeline.py:390-446 is split into W
-     equal contiguous ranges; each rank runs the 1-step UNet and the VAE decode of its range
-     (≈94 % of the FLOPs);
-  3. the decoded snippets are all-gathered (the north_star's all-gather of per-snippet depth
-     before co-alignment) and rank 0 runs the DepthAligner, the merge and the renormalisation.
-The arithmetic per snippet is identical to the single-GPU path (batching-invariant kernels),
-so sharded output == single-GPU output bitwise.
+     contiguous ranges of equal size (every snippet costs the same); each rank runs the 1-step UNet
+     and the VAE decode of its range (≈94 % of the FLOPs) and keeps the decoded snippets;
+  3. co-alignment (depth_aligner.py:68-120) without moving full-resolution depth:
+       all-reduce MIN of the local snippet minima (the shift of :78);
+       each rank crops / subsamples its own snippets (:82-92) and the [n, w, P] f32 aligner inputs
+       are all-gathered (3·P·4 B = 71 KB per snippet at 768², the north_star's all-gather of
+       per-snippet depth before co-alignment);
+       every rank runs the same deterministic 2000-iteration Adam kernel on the same inputs, so every
+       rank holds the same scales / translations with no broadcast;
+       merge_scaled_triplets (:231-262) as rank-local per-frame sums of s·x+t over the rank's own
+       full-resolution snippets, reduce-scatter SUM by frame chunk, ÷ the frame's cover count;
+       all-reduce MIN / MAX for the renormalisation (rollingdepth_pipeline.py:316-318);
+  4. refine (full / paper presets): each rank encodes its chunk of the co-aligned depth, the depth
+     latents are all-gathered, and every refine step splits its snippets over the ranks with one
+     all-reduce of the [N, h·w, 4] f32 per-frame sums (pipeline.refine(group=...)); each rank decodes
+     its own frame chunk of the refined latents.
+Outputs stay distributed: rank r holds depth / coaligned depth for frames chunk_bounds(N, W)[r]
+(and its own decoded snippets); `gather=True` assembles the full maps on every rank.
+
+Numerics vs the single-GPU forward: identical per-snippet arithmetic, but not bitwise — the kernel
+engine chosen per launch depends on the batch shape (f32 accumulation order), the merge / refine sums
+are reduced across ranks in RCCL's order, and the aligner runs on the same inputs but the snippets
+each rank batched differ.  Stated tolerance: depth mean |Δ| ≤ 1e-3 (the north_star bound) against
+the single-GPU result (tests/test_pipeline_gpu.py); with W = 1 the plan reproduces forward bitwise.
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
 
-F16 = torch.float16
+F16, F32 = torch.float16, torch.float32
 
 
 def chunk_bounds(total: int, world: int) -> List[Tuple[int, int]]:
@@ -32,7 +50,8 @@ def flat_snippets(counts: Sequence[int]) -> List[Tuple[int, int]]:
 
 
 def rank_subsets(counts: Sequence[int], world: int, rank: int) -> List[List[int]]:
-    """Snippet indices per dilation owned by `rank` under the contiguous flat split."""
+    """Snippet indices per dilation owned by `rank` under the contiguous flat split (contiguous
+    within each dilation)."""
     flat = flat_snippets(counts)
     lo, hi = chunk_bounds(len(flat), world)[rank]
     sub = [[] for _ in counts]
@@ -42,7 +61,7 @@ def rank_subsets(counts: Sequence[int], world: int, rank: int) -> List[List[int]
 
 
 def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) -> torch.Tensor:
-    """All-gather equal-size row chunks (padded) → [total, ...]."""
+    """All-gather the rows of chunk_bounds(total, world)[rank] from every rank → [total, ...]."""
     c = (total + world - 1) // world
     if local.shape[0] < c:
         pad = torch.zeros((c - local.shape[0], *local.shape[1:]), dtype=local.dtype, device=local.device)
@@ -52,42 +71,67 @@ def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) ->
     return out[:total]
 
 
-def local_rows(snippets: Sequence[torch.Tensor], counts: Sequence[int], world: int, rank: int) -> torch.Tensor:
-    """This rank's decoded snippets in flat (dilation, snippet) order → [rows, w, H, W]."""
-    flat = flat_snippets(counts)
-    lo, hi = chunk_bounds(len(flat), world)[rank]
-    ref = next(s for s in snippets if s is not None)
-    out = torch.empty((max(hi - lo, 0), *ref.shape[1:]), dtype=ref.dtype, device=ref.device)
-    for i, (d, k) in enumerate(flat[lo:hi]):
-        out[i] = snippets[d][k]
-    return out
+def _reduce_scatter_rows(full: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """SUM over ranks of `full` [total, ...], rank r keeping rows chunk_bounds(total, world)[r]."""
+    total = full.shape[0]
+    c = (total + world - 1) // world
+    if c * world != total:
+        full = torch.cat([full, torch.zeros((c * world - total, *full.shape[1:]), dtype=full.dtype,
+                                            device=full.device)])
+    out = torch.empty((c, *full.shape[1:]), dtype=full.dtype, device=full.device)
+    dist.reduce_scatter_tensor(out, full.contiguous(), group=group)
+    rank = dist.get_rank(group)
+    lo, hi = chunk_bounds(total, world)[rank]
+    return out[:hi - lo]
 
 
-def gather_snippets(local: torch.Tensor, counts: Sequence[int], world: int, group=None) -> List[torch.Tensor]:
-    """All-gather every rank's rows and split them back per dilation."""
-    allsn = _all_gather_rows(local, sum(counts), world, group)
+def gather_rows_by_dilation(local: Sequence[torch.Tensor], counts: Sequence[int], world: int,
+                            group=None) -> List[torch.Tensor]:
+    """Every rank's rows (its flat range, per dilation in `local`) all-gathered and split back
+    per dilation: → [n_d, ...] for every d."""
+    ref = next((t for t in local if t is not None), None)
+    flat_local = torch.cat([t for t in local if t is not None and t.shape[0]]) if any(
+        t is not None and t.shape[0] for t in local) else torch.zeros((0, *ref.shape[1:]), dtype=ref.dtype,
+                                                                      device=ref.device)
+    allrows = _all_gather_rows(flat_local, sum(counts), world, group)
     per_d, o = [], 0
     for n in counts:
-        per_d.append(allsn[o:o + n])
+        per_d.append(allrows[o:o + n])
         o += n
     return per_d
 
 
+def _all_reduce_minmax(mm: torch.Tensor, group=None) -> torch.Tensor:
+    """[min, max] f32 → the global [min, max] (one MIN all-reduce of [min, −max])."""
+    t = torch.stack([mm[0], -mm[1]])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return torch.stack([t[0], -t[1]])
+
+
+class ShardedOutput:
+    """Distributed RollingDepthOutput: this rank's frame chunk [f0, f1) of depth_pred /
+    depth_coaligned / input_rgb, its own decoded snippets (snippet_rows[d] are global snippets
+    snippet_k0[d] ..), and — when gathered — the full maps."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
 @torch.no_grad()
 def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool = True,
-                    snippet_len: int = 3, coalign_kwargs=None, init_noise: torch.Tensor = None, group=None,
-                    num_frames: int = None, to_host: bool = False):
-    """Multi-GPU RollingDepthPipeline.forward (refine_step = 0).  Returns the depth [N,1,H,W] f16
-    on rank 0 (None elsewhere) and the per-dilation snippets on rank 0.
+                    snippet_len: int = 3, coalign_kwargs=None, init_noise: Optional[torch.Tensor] = None, group=None,
+                    num_frames: Optional[int] = None, to_host: bool = False, refine_step: int = 0,
+                    refine_snippet_len: int = 3, refine_start_dilation: int = 6, gather: bool = False,
+                    record: Optional[dict] = None) -> ShardedOutput:
+    """Multi-GPU RollingDepthPipeline.forward (every preset: refine_step > 0 included).
 
-    `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N`
-    — only this rank's contiguous chunk chunk_bounds(N, world)[rank] (each rank then holds 1/W of
-    the video in host/device memory).
-
-    `to_host=True` mirrors forward()'s D2H boundary, distributed: every rank copies its own chunk
-    of input_rgb and its own snippet rows to pinned host memory (overlapping the gathers and the
-    aligner), rank 0 the coaligned depth; rank 0 returns (depth_host, per-dilation device
-    snippets), other ranks (None, None) — after their copies completed."""
+    `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N` —
+    only this rank's contiguous chunk chunk_bounds(N, world)[rank] (each rank then holds 1/W of the
+    video in host / device memory).  `to_host=True` mirrors forward()'s D2H boundary, distributed:
+    every rank copies its own depth / coaligned / input_rgb chunk and its own snippet rows to pinned
+    host memory.  `gather=True` also all-gathers the full depth_pred / depth_coaligned on every rank
+    (tests, small N).  `dilations` is not mutated (forward() mutates the caller's list; this is the
+    build's own entry point)."""
     from . import kernels as K
     from .aligner import DepthAligner
 
@@ -99,49 +143,91 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     dil = list(dilations)
     if cap_dilation:
         dil = [pipe.cap_max_dilation(N, snippet_len, d) for d in dil]
-    # 1. encode my frame chunk, all-gather latents
-    lo, hi = chunk_bounds(N, world)[rank]
-    f = pipe.vae.factor
-    H, W = frames.shape[-2:]
-    h, w = H // f, W // f
-    mine_frames = frames[lo:hi] if num_frames is None else frames
-    if num_frames is not None and mine_frames.shape[0] != hi - lo:
-        raise ValueError(f"rank {rank} holds {mine_frames.shape[0]} frames, expected {hi - lo}")
-    if hi > lo:
+        refine_start_dilation = pipe.cap_max_dilation(N, refine_snippet_len, refine_start_dilation)
+    if 1 not in dil:
+        raise AssertionError("dilations should include 1")
+    f0, f1 = chunk_bounds(N, world)[rank]
+    mine_frames = frames[f0:f1] if num_frames is None else frames
+    if num_frames is not None and mine_frames.shape[0] != f1 - f0:
+        raise ValueError(f"rank {rank} holds {mine_frames.shape[0]} frames, expected {f1 - f0}")
+    H_in, W_in = frames.shape[-2:]
+    h, w = pipe.vae.latent_hw(H_in, W_in)
+    # 1. encode my frame chunk, all-gather the latents
+    if f1 > f0:
         mine = pipe.encode_rgb(mine_frames.to(dev))
     else:
-        mine = torch.zeros((0, h, w, 8), dtype=F16, device=dev)
+        mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=F16, device=dev)
     rgb_latent = _all_gather_rows(mine, N, world, group)
     if init_noise is None:
         g = torch.Generator(device=dev).manual_seed(0)
         init_noise = torch.randn((1, 4, h, w), device=dev, dtype=F16, generator=g)
-    noise = K.nchw_to_nhwc(init_noise.to(dev), 8)
-    # 2. my snippets
+    noise = pipe._noise_nhwc(init_noise, h, w)
+    # 2. my snippets (compact: row r of dilation d is global snippet subsets[d][r])
     counts = [len(pipe.get_snippet_indice(0, [0], N, snippet_len, d, d, 1)) for d in dil]
     subsets = rank_subsets(counts, world, rank)
-    snippets = pipe.init_snippet_infer(rgb_latent, noise, dil, [snippet_len] * len(dil), [1] * len(dil),
-                                       [1] * len(dil), snippet_subset=subsets)
-    local = local_rows(snippets, counts, world, rank)
+    k0 = [s[0] if s else 0 for s in subsets]
+    rows = pipe.init_snippet_infer(rgb_latent, noise, dil, [snippet_len] * len(dil), [1] * len(dil), [1] * len(dil),
+                                   snippet_subset=subsets)
+    H, W = rows[0].shape[-2:]
     d2h = torch.cuda.Stream(dev) if to_host else None
-    if to_host:
-        for t in local:
-            if t.shape[0]:
-                pipe._to_host_async(t, d2h)
-        if hi > lo:
-            pipe._to_host_async(mine_frames.to(dev, F16) / 2.0 + 0.5, d2h)
-    # 3. all-gather decoded snippets, co-align on rank 0
-    per_d = gather_snippets(local, counts, world, group)
-    if rank != 0:
-        if d2h is not None:
-            d2h.synchronize()
-        return None, None
+    snip_host = [pipe._to_host_async(r, d2h) if r.shape[0] else None for r in rows] if to_host else None
+    # 3. co-alignment
     aligner = DepthAligner(device=dev, **(coalign_kwargs or {}))
-    merged, _, _, _ = aligner.run([s.view(s.shape[0], snippet_len, 1, H, W) for s in per_d], dil)
-    d = merged.float().contiguous()
-    K.renormalize_(d, K.minmax(d))
-    depth = d.to(F16)
-    if d2h is not None:
-        depth = pipe._to_host_async(depth, d2h)
-        pipe._to_host_async(d.to(F16), d2h)  # depth_pred (== coaligned without refine)
+    local_mm = [K.minmax(r) for r in rows if r.shape[0]]
+    mm = K.minmax(torch.stack(local_mm).reshape(-1)) if local_mm else \
+        torch.tensor([float("inf"), float("-inf")], device=dev)
+    shift = _all_reduce_minmax(mm, group)  # shift[0] = global min
+    prepared = [aligner.prepare([r], shift)[0] if r.shape[0] else None for r in rows]
+    P = ((H - 2 * aligner.border + aligner.factor - 1) // aligner.factor) * \
+        ((W - 2 * aligner.border + aligner.factor - 1) // aligner.factor)
+    proto = torch.empty((0, snippet_len, P), dtype=F32, device=dev)
+    xs = gather_rows_by_dilation([p if p is not None else proto for p in prepared], counts, world, group)
+    strides = list(dil)
+    seq_len = aligner.sequence_length(counts, snippet_len, dil)
+    assert seq_len == N
+    scales, trans, hist, ws = aligner.optimize_prepared(xs, strides, N)
+    sums = K.aligner_merge_partial([r if r.shape[0] else None for r in rows], k0, counts, scales, trans, strides,
+                                   snippet_len, N, H * W, shift, x_f32=False)
+    my_sums = _reduce_scatter_rows(sums, world, group)
+    merged = K.aligner_merge_finish(my_sums, counts, strides, snippet_len, f0) if f1 > f0 else my_sums
+    d = merged.to(F16).float().contiguous()  # merge_scaled_triplets returns the snippets' dtype
+    mm_d = K.minmax(d) if d.numel() else torch.tensor([float("inf"), float("-inf")], device=dev)
+    gmm = _all_reduce_minmax(mm_d, group)
+    if d.numel():
+        K.renormalize_(d, gmm)
+    coaligned = d.to(F16).view(f1 - f0, 1, H, W)
+    del ws
+    # 4. refine
+    if refine_step > 0:
+        if f1 > f0:
+            dlat_mine = pipe.encode_rgb(coaligned.expand(-1, 3, -1, -1))
+        else:
+            dlat_mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=F16, device=dev)
+        dlat = _all_gather_rows(dlat_mine, N, world, group)
+        new = pipe.refine(rgb_latent, dlat, noise, refine_step, refine_snippet_len, refine_start_dilation,
+                          group=group)
+        if record is not None:
+            record["refined_latent"] = new
+        depth = torch.empty((f1 - f0, H, W, 1), dtype=F16, device=dev)
+        if f1 > f0:
+            z = K.ddim_combine(new[f0:f1, ..., :4], new[f0:f1, ..., :4], 1.0 / pipe.depth_latent_scale_factor, 0.0,
+                               1.0, 4, 8)
+            pipe.decode_depth(z, depth)
+        depth = depth.view(f1 - f0, 1, H, W)
+    else:
+        depth = coaligned
+    if record is not None:
+        record.update(rgb_latent=rgb_latent, scales=scales, translations=trans, dilations=list(dil),
+                      loss_history=hist)
+    out = ShardedOutput(frame_range=(f0, f1), depth_pred=depth, depth_coaligned=coaligned, snippet_rows=rows,
+                        snippet_k0=k0, snippet_counts=counts, dilations=dil, input_rgb=None, snippet_host=snip_host)
+    if gather:
+        out.depth_pred_full = _all_gather_rows(depth, N, world, group)
+        out.depth_coaligned_full = _all_gather_rows(coaligned, N, world, group)
+    if to_host:
+        out.depth_pred = pipe._to_host_async(depth, d2h)
+        out.depth_coaligned = pipe._to_host_async(coaligned, d2h) if refine_step > 0 else out.depth_pred
+        if f1 > f0:
+            out.input_rgb = pipe._to_host_async(mine_frames.to(dev, F16) / 2.0 + 0.5, d2h)
         d2h.synchronize()
-    return depth, per_d
+    return out

@@ -112,6 +112,47 @@ def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, 
     print(name, {k: tuple(v.shape) for k, v in t.items()})
 
 
+def _h16(t):
+    return t.detach().to(torch.float16).contiguous().clone()
+
+
+def compact_fixture(P, name, ucfg, vcfg, n, res, dilations, cap, depth_stride, refine_step=0, refine_start=6):
+    """Large-resolution fixture (768² / 1024²) kept small enough to commit: the frames are NOT
+    stored (the GPU test re-synthesises them with weights.synth_frames(n, res, res, seed=0), bitwise
+    the same tensor), latents are stored in f16 (the HIP path stores f16), only the first snippet of
+    each dilation is stored, and depth maps are stored f16 on a [::s, ::s] pixel lattice plus the
+    full-map mean / mean-|x| (size-independent checksums of the whole map)."""
+    pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
+    frames = W.synth_frames(n, res, res, seed=0)
+    h = w = res // C.vae_downscale(vcfg)
+    noise = torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(1))
+    out, rec = run_pipe(pipe, frames, dilations, cap, 1, None, refine_step, refine_start)
+    s = depth_stride
+    t = {
+        "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
+        "frames_checksum": torch.tensor([frames.double().sum().item(), frames.double().abs().sum().item()]),
+        "rgb_latent": _h16(rec["rgb_latent"]),
+        "unet_out_first": _h16(rec["unet_out"][0]), "unet_out_last": _h16(rec["unet_out"][-1]),
+        "depth_pred_sub": _h16(out.depth_pred[..., ::s, ::s]),
+        "depth_coaligned_sub": _h16(out.depth_coaligned[..., ::s, ::s]),
+        "depth_pred_stats": torch.tensor([out.depth_pred.double().mean().item(),
+                                          out.depth_pred.double().abs().mean().item()]),
+    }
+    if refine_step > 0:
+        t["refined_latent"] = _h16(rec["snip_lat"][-1][0])
+    for i, sn in enumerate(out.snippet_ls):
+        t[f"snippet_latent_{i}_first"] = _h16(rec["snip_lat"][i][0])
+        t[f"snippet_{i}_first_sub"] = _h16(sn[0, :, 0, ::s, ::s])
+        t[f"snippet_{i}_stats"] = torch.tensor([sn.double().mean().item(), sn.double().abs().mean().item()])
+    save_file(t, os.path.join(HERE, name + ".safetensors"))
+    meta = {"n_frames": n, "res": res, "frames_seed": 0, "depth_stride": s, "dilations_in": list(dilations),
+            "dilations_used": rec["dilations_used"], "cap_dilation": cap, "unet": ucfg, "vae": vcfg,
+            "scheduler": C.RD_SCHEDULER, "coalign": {}, "refine_step": refine_step,
+            "refine_start_dilation": refine_start, "n_unet_calls": len(rec["unet_out"])}
+    json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
+    print(name, {k: tuple(v.shape) for k, v in t.items()}, flush=True)
+
+
 def attn_fixture():
     from diffusers.models.attention_processor import Attention, AttnProcessor2_0
 
@@ -240,7 +281,7 @@ def main():
     ap.add_argument("--skip-sd2", action="store_true")
     ap.add_argument("--only", default="")
     a = ap.parse_args()
-    torch.set_num_threads(os.cpu_count() or 8)
+    torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", os.cpu_count() or 8)))
     P, A = _refload.load_reference()
     todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "sd2"]
     if "keys" in todo:
@@ -263,6 +304,17 @@ def main():
     if "sd2" in todo and not a.skip_sd2:
         frames = W.synth_frames(3, 256, 256, seed=0)
         pipeline_fixture(P, "sd2_256", C.SD2_UNET, C.SD2_VAE, frames, [1], False)
+    # large-resolution fixtures (opt-in: --only; tens of CPU-minutes each)
+    if "sd2_768" in todo:  # fast preset arithmetic on one 3-frame 768² snippet (SURVEY §8c fixture 3)
+        compact_fixture(P, "sd2_768", C.SD2_UNET, C.SD2_VAE, 3, 768, [1], False, 2)
+    if "sd2_1024" in todo:  # fast1024 preset arithmetic on one 3-frame 1024² snippet
+        compact_fixture(P, "sd2_1024", C.SD2_UNET, C.SD2_VAE, 3, 1024, [1], False, 2)
+    if "full1024" in todo:  # full preset: 1024², [1,10,25] capped as the reference caps, refine 10
+        compact_fixture(P, "full1024", C.SD2_UNET, C.SD2_VAE, 6, 1024, [1, 10, 25], True, 4, refine_step=10,
+                        refine_start=6)
+    if "paper256" in todo:  # paper preset semantics (fp32, cap_dilation False, refine 10) at 256², N=51
+        compact_fixture(P, "paper256", C.SD2_UNET, C.SD2_VAE, 51, 256, [1, 10, 25], False, 2, refine_step=10,
+                        refine_start=6)
 
 
 if __name__ == "__main__":

@@ -307,6 +307,25 @@ def test_attention_fused_qkv(B, S, H):
     assert (o.float() - ref).abs().max().item() < 5e-3
 
 
+@pytest.mark.parametrize("B,S,H", [(2, 27648, 5), (1, 49152, 5)])
+def test_attention_pipeline_sizes_sampled_rows(B, S, H):
+    """Level-0 cross-frame attention at the metric config (768²: S = 3·96² = 27 648, H = 5) and at
+    1024² (S = 3·128² = 49 152), QKV as the fused projection writes it, against fp32 SDPA over all
+    keys for 512 sampled query rows per snippet (the full fp32 reference would need S² scores)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(21)
+    C = H * 64
+    qkv = (torch.randn(B, S, 3 * C, device=DEV, generator=g) * 0.7).half()
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    o = K_.attention(q, k, v, H)
+    rows = torch.randint(0, S, (512,), device=DEV, generator=g)
+    ref = _sdpa_ref(q[:, rows].contiguous(), k, v, H)
+    err = (o[:, rows].float() - ref).abs()
+    print(f"S={S}: max {err.max().item():.2e} mean {err.mean().item():.2e}")
+    assert torch.isfinite(o).all()
+    assert err.max().item() < 5e-3 and err.mean().item() < 5e-4
+
+
 def test_attention_softmax_rescale_branch():
     """A key spike late in the sequence forces the running-max rescale (guide rule 26)."""
     K_ = _k()

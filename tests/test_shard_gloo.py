@@ -1,9 +1,17 @@
-"""World-size-2 gloo test (CPU) of the multi-GPU collective plan of rollingdepth_amd/shard.py:
-each rank produces only its contiguous flat range of snippets, the all-gather + per-dilation
-split must reassemble exactly the single-process snippet lists (and latents for the frame split)."""
+"""World-size-2 (and 3) gloo tests (CPU) of the multi-GPU plan of rollingdepth_amd/shard.py
+(SURVEY.md §8e).  The collectives and the rank/frame/snippet bookkeeping are the product's own
+functions; the per-rank device kernels (rdmi_aligner_merge_partial / rdmi_snippet_accumulate) are
+stood in for by a CPU restatement of their contract (the GPU tests check the kernels against the
+single-GPU merge and refine).  Checked against the oracle's single-process merge / refine average:
+  * the flat snippet split + all-gather of per-snippet aligner inputs reassembles every dilation;
+  * all-reduce MIN of [min, −max] gives the global min / max;
+  * per-rank merge sums + reduce-scatter by frame + ÷ cover count == merge_scaled_triplets;
+  * per-rank refine sums + all-reduce + ÷ cover count == the single-process snippet average.
+"""
 import os
 import socket
 
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -21,38 +29,113 @@ def _snippet(d, k, shape):
     return torch.full(shape, float(1000 * d + k)) + torch.arange(shape[-1]).float()
 
 
-def _worker(rank, world, port, counts, res):
+def _merge_partial_cpu(rows, k0, n, strides, scales, trans, w, N, HW):
+    """CPU restatement of rdmi_aligner_merge_partial (f32 snippets): per frame the sum over this
+    rank's (dilation, local snippet, slot) of s·x + t, slots in the reference's k-ascending order."""
+    out = torch.zeros((N, HW), dtype=torch.float32)
+    for f in range(N):
+        acc = torch.zeros(HW, dtype=torch.float32)
+        for d, r in enumerate(rows):
+            for j in range(w - 1, -1, -1):
+                k = f - j * strides[d]
+                if k < k0[d] or k >= k0[d] + r.shape[0]:
+                    continue
+                acc = acc + (r[k - k0[d], j].reshape(-1) * scales[d][k] + trans[d][k])
+        out[f] = acc
+    return out
+
+
+def _cover(n, strides, w, f):
+    return sum(1 for d in range(len(n)) for j in range(w) if 0 <= f - j * strides[d] < n[d])
+
+
+def _worker(rank, world, port, res):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from rollingdepth_amd.shard import _all_gather_rows, chunk_bounds, gather_snippets, local_rows, rank_subsets
+    from oracle import rd_oracle as O
+    from rollingdepth_amd.shard import (_all_gather_rows, _all_reduce_minmax, _reduce_scatter_rows, chunk_bounds,
+                                        gather_rows_by_dilation, rank_subsets)
 
+    ok = True
+    # --- flat split + all-gather of per-snippet rows (the aligner inputs) -----------------------
+    counts = [9, 5]
     shape = (3, 2, 5)
     sub = rank_subsets(counts, world, rank)
-    snippets = []
-    for d, n in enumerate(counts):
-        buf = torch.full((n, *shape), -1.0)
-        for k in sub[d]:
-            buf[k] = _snippet(d, k, shape)
-        snippets.append(buf)
-    per_d = gather_snippets(local_rows(snippets, counts, world, rank), counts, world)
-    ok = all(torch.equal(per_d[d][k], _snippet(d, k, shape)) for d, n in enumerate(counts) for k in range(n))
+    local = [torch.stack([_snippet(d, k, shape) for k in sub[d]]) if sub[d] else torch.zeros((0, *shape))
+             for d in range(len(counts))]
+    per_d = gather_rows_by_dilation(local, counts, world)
+    ok &= all(torch.equal(per_d[d][k], _snippet(d, k, shape)) for d, n in enumerate(counts) for k in range(n))
+    # every rank's subset is contiguous within a dilation (compact rows = global k0 ..)
+    ok &= all(s == list(range(s[0], s[0] + len(s))) for s in sub if s)
+    # --- frame-chunk latents all-gather ------------------------------------------------------------
     N = 11
     lo, hi = chunk_bounds(N, world)[rank]
     lat = _all_gather_rows(torch.arange(lo, hi).float().view(-1, 1).expand(-1, 4).contiguous(), N, world)
-    ok = ok and torch.equal(lat[:, 0], torch.arange(N).float())
+    ok &= torch.equal(lat[:, 0], torch.arange(N).float())
+    # --- global min / max -----------------------------------------------------------------------------
+    mm = _all_reduce_minmax(torch.tensor([float(rank) - 5.0, 10.0 * rank]))
+    ok &= mm.tolist() == [-5.0, 10.0 * (world - 1)]
+    # --- merge: rank-local sums, reduce-scatter by frame, ÷ cover count == merge_scaled_triplets -----
+    N, w, H, W = 14, 3, 4, 5
+    dil = [1, 4]
+    g = torch.Generator().manual_seed(11)
+    full = [torch.rand((N - (w - 1) * d, w, H, W), generator=g) for d in dil]
+    n = [x.shape[0] for x in full]
+    sc = [0.5 + torch.rand(m, generator=g) for m in n]
+    tr = [0.1 * torch.randn(m, generator=g) for m in n]
+    sub = rank_subsets(n, world, rank)
+    k0 = [s[0] if s else 0 for s in sub]
+    rows = [full[d][k0[d]:k0[d] + len(sub[d])] for d in range(len(dil))]
+    sums = _merge_partial_cpu(rows, k0, n, dil, sc, tr, w, N, H * W)
+    mine = _reduce_scatter_rows(sums, world)
+    f0, f1 = chunk_bounds(N, world)[rank]
+    merged_mine = torch.stack([mine[i] / _cover(n, dil, w, f0 + i) for i in range(f1 - f0)]) if f1 > f0 else mine
+    merged = _all_gather_rows(merged_mine, N, world)
+    idx = [O.aligner_indices(N, d - 1, w) for d in dil]
+    ref = O.aligner_merge([x.numpy()[:, :, None] for x in full], idx, [s.numpy() for s in sc],
+                          [t.numpy() for t in tr], N)
+    err = np.abs(merged.numpy() - ref.reshape(N, H * W)).max()
+    ok &= bool(err < 1e-5)
+    # --- refine step: rank-local sums of its snippets' predictions, all-reduce, ÷ cover count ---------
+    Nf, L, P, C = 13, 3, 6, 4
+    stride = 2
+    nsn = Nf - (L - 1) * stride
+    preds = torch.randn((nsn, L, P, C), generator=g)
+    a, b = chunk_bounds(nsn, world)[rank]
+    acc = torch.zeros((Nf, P, C))
+    for s in range(a, b):
+        for j in range(L):
+            acc[s + j * stride] += preds[s, j]
+    dist.all_reduce(acc)
+    cnt = torch.tensor([sum(1 for j in range(L) if 0 <= f - j * stride < nsn) for f in range(Nf)]).float()
+    got = acc / cnt[:, None, None]
+    want = torch.zeros((Nf, P, C))
+    for s in range(nsn):
+        for j in range(L):
+            want[s + j * stride] += preds[s, j]
+    want /= cnt[:, None, None]
+    ok &= torch.allclose(got, want, atol=1e-6)
     res[rank] = int(ok)
     dist.destroy_process_group()
 
 
-def test_gather_reassembles_single_process_layout():
-    world = 2
+def _run(world):
     ctx = mp.get_context("spawn")
     res = ctx.Array("i", [0] * world)
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, [9, 5], res)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, res)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(120)
+        p.join(180)
     assert all(p.exitcode == 0 for p in procs)
     assert list(res) == [1] * world
+
+
+def test_shard_plan_world2():
+    _run(2)
+
+
+def test_shard_plan_world3():
+    """An uneven split (ragged last chunks) — the same plan at W = 3."""
+    _run(3)
