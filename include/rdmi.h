@@ -65,6 +65,10 @@ typedef struct rdmi_gemm_args {
    * gn_part[v * gn_ld + 2*r + {0,1}] = (Σ, Σ²) over output rows 32r..32r+31 and channels
    * 4v..4v+3, summed in a fixed order (rdmi_groupnorm_stats_partials consumes them).  NULL: off. */
   float* gn_part; long gn_ld;
+  /* storage dtype of A, W, C and residual: RDMI_F16 (f16 MFMA, f32 accumulate; C f32 when c_f32) or
+   * RDMI_F32 (the paper preset: f32-input MFMA v_mfma_f32_16x16x4_f32, exact f32 products, C / residual
+   * f32; K % 4 == 0; no GroupNorm moments) */
+  int dtype;
 } rdmi_gemm_args;
 int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
 
@@ -94,47 +98,51 @@ typedef struct rdmi_conv_args {
    * padding still zero; the same values rdmi_groupnorm_apply writes.  NULL in_mean_rstd: off.
    * Shapes that support it: rdmi_conv2d_in_gn_supported (otherwise RDMI_E_UNSUPPORTED). */
   const float* in_mean_rstd; const float* in_gamma; const float* in_beta; int in_groups, in_silu;
+  /* RDMI_F16 or RDMI_F32 (x, w, y, residual).  f32 weights are always [Cout][kh][kw][Cin] (tap-major,
+   * Kp % 32 == 0), Cin % 4 == 0, no input GroupNorm and no GroupNorm moments. */
+  int dtype;
 } rdmi_conv_args;
 int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
 /* 1 if rdmi_conv2d fuses an input GroupNorm for this shape (in_groups set; pointers not read) */
 int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* args);
 
 /* ---------------------------------------------------------------------------------------
- * GroupNorm on NHWC f16: statistics then apply (optionally fused SiLU).
+ * GroupNorm on NHWC f16 / f32 (dtype RDMI_F16 / RDMI_F32): statistics then apply (optionally fused SiLU).
  * Replaces F.group_norm (+ SiLU) of ResnetBlock2D.norm1/norm2 (resnet.py:326,351),
  * Transformer2DModel.norm (transformer_2d.py:175-177), conv_norm_out of UNet/VAE, and the VAE
  * mid-block Attention.group_norm (attention_processor.py:2221-2222).
  * stats: mean_rstd[b*G + g] = {mean, rstd}; workspace ≥ rdmi_groupnorm_workspace(B, G) floats.
  */
 long rdmi_groupnorm_workspace(int B, int G);
-int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G, float eps,
+int rdmi_groupnorm_stats(const void* x, int dtype, int B, long HW, int C, int G, float eps,
                          float* mean_rstd, float* workspace, void* stream);
 /* Statistics from the 32-row × 4-channel moments a producing GEMM/conv emitted (gn_part): for
  * image b (rows b·HW .. b·HW+HW-1, HW % 32 == 0) and group g ((C/G) % 4 == 0), an f64 sum over the
  * group's partials in a fixed order — independent of how many images share the tensor. */
 int rdmi_groupnorm_stats_partials(const float* part, long part_ld, int B, long HW, int C, int G, float eps,
                                   float* mean_rstd, void* stream);
-int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G,
+int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, long HW, int C, int G,
                          const float* mean_rstd, const float* gamma, const float* beta, int silu,
                          void* stream);
 
 /* GroupNorm apply (+ SiLU when silu = 1) fused with a 3×3, stride-1, pad-1 convolution to ONE output
  * channel: y[b, h, w] = bias + Σ_{dy,dx,c} w[3dy+dx][c] · n(x)[b, h+dy-1, w+dx-1, c], n = the
- * normalised (+SiLU) input, zero outside the image.  x [B][H][W][C] f16, w [9][C] f32, y [B][H][W]
- * f16, workspace ≥ rdmi_conv3x3_to1_gn_workspace(B, H, W) floats.  Replaces the decoder's
+ * normalised (+SiLU) input, zero outside the image.  x [B][H][W][C] and y [B][H][W] in `dtype`
+ * (RDMI_F16 / RDMI_F32), w [9][C] f32, workspace ≥ rdmi_conv3x3_to1_gn_workspace(B, H, W) floats.  Replaces the decoder's
  * conv_norm_out → conv_act → conv_out (vae.py:335-347) followed by the depth pipeline's mean over
  * the RGB outputs (rollingdepth_pipeline.py:737), which is linear and folded into w / bias. */
 long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W);
-int rdmi_conv3x3_to1_gn(const void* x, int B, int H, int W, int C, int G, const float* mean_rstd,
+int rdmi_conv3x3_to1_gn(const void* x, int dtype, int B, int H, int W, int C, int G, const float* mean_rstd,
                         const float* gamma, const float* beta, int silu, const float* w, float bias,
                         void* y, float* workspace, void* stream);
 
 /* LayerNorm over the last dim (BasicTransformerBlock.norm1/2/3, attention.py:445,495,522). */
-int rdmi_layernorm(const void* x, void* y, long M, int C, const float* gamma, const float* beta,
+int rdmi_layernorm(const void* x, void* y, int dtype, long M, int C, const float* gamma, const float* beta,
                    float eps, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * Fused multi-head attention forward, softmax(q kᵀ · scale) v, non-causal, no mask, D = 64.
+ * Fused multi-head attention forward, softmax(q kᵀ · scale) v, non-causal, no mask, D = 64; dtype
+ * RDMI_F16 (f16 MFMA, f32 softmax) or RDMI_F32 (f32-input MFMA, f32 softmax; the paper preset).
  * Token-major q/k/v/o with row strides (ld*) and batch strides (bs*), head h at column h*D.
  * With the num_view fold done by the caller's strides (one "batch" = one snippet of n frames,
  * S = n·h·w), this is the cross-frame self-attention of the modified AttnProcessor2_0
@@ -142,13 +150,13 @@ int rdmi_layernorm(const void* x, void* y, long M, int C, const float* gamma, co
  */
 int rdmi_attention_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq,
                        int Sk, int D, long q_ld, long k_ld, long v_ld, long o_ld, long q_bs,
-                       long k_bs, long v_bs, long o_bs, float scale, void* stream);
+                       long k_bs, long v_bs, long o_bs, float scale, int dtype, void* stream);
 
 /* Attention against a short key set (L ≤ 16 keys, e.g. the 2-token empty-text context of the
  * UNet cross-attention attn2, attention.py:508-516); k/v [Bkv][L][H*D] contiguous, Bkv ∈ {1, B}. */
 int rdmi_attention_smallkv(const void* q, const void* k, const void* v, void* o, int B, int H,
                            int Sq, int L, int D, long q_ld, long o_ld, long q_bs, long o_bs,
-                           long kv_bs, float scale, void* stream);
+                           long kv_bs, float scale, int dtype, void* stream);
 
 /* BasicTransformerBlock's norm2 → attn2 → +residual against a TWO-token shared context
  * (attention.py:480-492, attention_processor.py:2172-2276 with Sk = 2), collapsed by exact algebra:
@@ -159,50 +167,54 @@ int rdmi_cross_attn_pair(const void* x, void* y, long M, int C, int H, const flo
                          const float* ln_beta, float eps, const float* w, const float* u, const float* c,
                          void* stream);
 
-/* Row softmax: p[r, :] = softmax(scale * s[r, :]) (f32 in, f16 out).  Used with two rdmi_gemm
+/* Row softmax: p[r, :] = softmax(scale * s[r, :]) (f32 in, p_dtype out: RDMI_F16 / RDMI_F32).  Used with two rdmi_gemm
  * calls for the single-head d=C VAE mid-block attention (unet_2d_blocks.py:680-697). */
 /* p[r·p_ld + c] = softmax_c(scale·s[r·cols + c]) for c < cols, 0 for cols ≤ c < p_ld (so a PV GEMM
  * can run on K = p_ld, a multiple of 8, when the key count is not). */
-int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, void* stream);
+int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, int p_dtype,
+                      void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Layout / elementwise helpers (f16 NHWC unless stated)
  */
 /* NCHW (f32 if x_f32 else f16, batch/channel strides in elements; x_cstride = 0 replicates one
  * channel, e.g. the depth → 3-channel repeat before re-encoding, rollingdepth_pipeline.py:327)
- * → NHWC f16 with channel padding to Cpad (zeros), y = x*scale */
-int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int B, int C, int H, int W, int Cpad,
+ * → NHWC in y_dtype (RDMI_F16 / RDMI_F32) with channel padding to Cpad (zeros), y = x*scale */
+int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int y_dtype, int B, int C, int H, int W, int Cpad,
                       float scale, long x_bstride, long x_cstride, void* stream);
-/* NHWC f16 (ld = channel stride) → NCHW f32, first C channels, y = x*scale + shift */
-int rdmi_nhwc_to_nchw_f32(const void* x, long ld, float* y, int B, int C, int H, int W,
+/* NHWC in dtype (ld = channel stride) → NCHW f32, first C channels, y = x*scale + shift */
+int rdmi_nhwc_to_nchw_f32(const void* x, int dtype, long ld, float* y, int B, int C, int H, int W,
                           float scale, float shift, void* stream);
-/* y[p, 0:Ca] = a[p, :], y[p, Ca:Ca+Cb] = b[p, :]  (torch.cat dim=1 of CrossAttn/UpBlock skips) */
-int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, void* stream);
+/* The helpers below take the storage dtype (RDMI_F16 / RDMI_F32) of every activation operand. */
+/* y[p, 0:Ca] = a[p, :], y[p, Ca:Ca+Cb] = b[p, :]  (torch.cat dim=1 of CrossAttn/UpBlock skips);
+ * Ca, Cb multiples of one 16-B vector (8 f16 / 4 f32) */
+int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, int dtype, void* stream);
 /* NHWC f16 nearest resize to an explicit size: y[b,yo,xo] = x[b, ⌊yo·H/Ho⌋, ⌊xo·W/Wo⌋] (f32 scale,
  * clamped) — F.interpolate(size=…, mode="nearest") of Upsample2D when the UNet forwards an
  * upsample size (latent not a multiple of 2^levels; unet_2d_condition.py forward_upsample_size,
  * upsampling.py:167-178).  C % 8 == 0. */
-int rdmi_resize_nearest(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo, void* stream);
-/* 2-D transpose per batch: dst[b][c][r] = src[b][r][c] (f16) */
+int rdmi_resize_nearest(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo, int dtype,
+                        void* stream);
+/* 2-D transpose per batch: dst[b][c][r] = src[b][r][c] */
 int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, long src_ld,
-                   long dst_ld, void* stream);
+                   long dst_ld, int dtype, void* stream);
 /* Build the 8-channel UNet input of single_step (rollingdepth_pipeline.py:646-651):
  * out[i, p, 0:4] = rgb[frame_idx[i], p, 0:4], out[i, p, 4:8] = depth[dsel(i), p, 0:4]
  * (depth_ld: frame stride of `depth` in elements; depth_bcast=1 uses depth frame 0 for all). */
 int rdmi_gather_unet_input(const void* rgb, long rgb_frame_ld, const void* depth,
                            long depth_frame_ld, int depth_bcast, const int* frame_idx, int count,
-                           long HW, void* out, void* stream);
+                           long HW, void* out, int dtype, void* stream);
 /* DDIM step (eta = 0) / add_noise as the affine map they reduce to (scheduling_ddim.py:402-448,
  * :471-495): y = (ca·x + cb·e) * out_scale; x, e: [P] pixel rows with strides, y [P, ld_y]
  * channels 0..C-1, channels C..Cpad-1 of y zeroed; e_period > 0 broadcasts e over pixel rows
  * (the shared init noise of every frame, :282-288). */
 int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* y, long ld_y,
                       long P, int C, int Cpad, float ca, float cb, float out_scale, long e_period,
-                      void* stream);
+                      int dtype, void* stream);
 /* Refine averaging (rollingdepth_pipeline.py:586-629): out[f] = mean over the snippets s = f − j·stride
  * (0 ≤ s < n) of src[s][j]; src [n][w][P][ld], out [N][P][ld] f16 (channels ≥ C zeroed). */
 int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld,
-                         void* out, void* stream);
+                         void* out, int dtype, void* stream);
 /* Sharded refine averaging (the loop above split over ranks): sum [N][P][C] f32 =
  * per frame the sum over THIS rank's snippets k0 .. k0+nloc-1 (src [nloc][w][P][ld], dtype RDMI_F16 /
  * RDMI_F32), zero where none covers the frame; after an all-reduce SUM over ranks,

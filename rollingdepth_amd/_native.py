@@ -29,6 +29,7 @@ class GemmArgs(C.Structure):
         ("M", i32), ("N", i32), ("K", i32), ("batch", i32),
         ("epilogue", i32),
         ("gn_part", vp), ("gn_ld", i64),
+        ("dtype", i32),
     ]
 
 
@@ -42,6 +43,7 @@ class ConvArgs(C.Structure):
         ("y_ld", i64), ("res_ld", i64), ("alpha", f32), ("rowbias_ld", i64),
         ("gn_part", vp), ("gn_ld", i64),
         ("in_mean_rstd", vp), ("in_gamma", vp), ("in_beta", vp), ("in_groups", i32), ("in_silu", i32),
+        ("dtype", i32),
     ]
 
 
@@ -66,25 +68,25 @@ _SIGS = {
     "rdmi_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
     "rdmi_conv2d_in_gn_supported": (i32, [C.POINTER(ConvArgs)]),
     "rdmi_groupnorm_workspace": (i64, [i32, i32]),
-    "rdmi_groupnorm_stats": (i32, [vp, i32, i64, i32, i32, f32, vp, vp, vp]),
+    "rdmi_groupnorm_stats": (i32, [vp, i32, i32, i64, i32, i32, f32, vp, vp, vp]),
     "rdmi_groupnorm_stats_partials": (i32, [vp, i64, i32, i64, i32, i32, f32, vp, vp]),
-    "rdmi_groupnorm_apply": (i32, [vp, vp, i32, i64, i32, i32, vp, vp, vp, i32, vp]),
+    "rdmi_groupnorm_apply": (i32, [vp, vp, i32, i32, i64, i32, i32, vp, vp, vp, i32, vp]),
     "rdmi_conv3x3_to1_gn_workspace": (i64, [i32, i32, i32]),
-    "rdmi_conv3x3_to1_gn": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, f32, vp, vp, vp]),
-    "rdmi_layernorm": (i32, [vp, vp, i64, i32, vp, vp, f32, vp]),
+    "rdmi_conv3x3_to1_gn": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, f32, vp, vp, vp]),
+    "rdmi_layernorm": (i32, [vp, vp, i32, i64, i32, vp, vp, f32, vp]),
     "rdmi_attention_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i64, i64, i64,
-                                 f32, vp]),
-    "rdmi_attention_smallkv": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, f32, vp]),
+                                 f32, i32, vp]),
+    "rdmi_attention_smallkv": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, f32, i32, vp]),
     "rdmi_cross_attn_pair": (i32, [vp, vp, i64, i32, i32, vp, vp, f32, vp, vp, vp, vp]),
-    "rdmi_softmax_rows": (i32, [vp, vp, i64, i64, i64, f32, vp]),
-    "rdmi_nchw_to_nhwc": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, f32, i64, i64, vp]),
-    "rdmi_nhwc_to_nchw_f32": (i32, [vp, i64, vp, i32, i32, i32, i32, f32, f32, vp]),
-    "rdmi_concat_channels": (i32, [vp, i32, vp, i32, vp, i64, vp]),
-    "rdmi_resize_nearest": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, vp]),
-    "rdmi_transpose": (i32, [vp, vp, i32, i64, i64, i64, i64, vp]),
-    "rdmi_gather_unet_input": (i32, [vp, i64, vp, i64, i32, vp, i32, i64, vp, vp]),
-    "rdmi_ddim_combine": (i32, [vp, i64, vp, i64, vp, i64, i64, i32, i32, f32, f32, f32, i64, vp]),
-    "rdmi_snippet_average": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, vp]),
+    "rdmi_softmax_rows": (i32, [vp, vp, i64, i64, i64, f32, i32, vp]),
+    "rdmi_nchw_to_nhwc": (i32, [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, i64, i64, vp]),
+    "rdmi_nhwc_to_nchw_f32": (i32, [vp, i32, i64, vp, i32, i32, i32, i32, f32, f32, vp]),
+    "rdmi_concat_channels": (i32, [vp, i32, vp, i32, vp, i64, i32, vp]),
+    "rdmi_resize_nearest": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, i32, vp]),
+    "rdmi_transpose": (i32, [vp, vp, i32, i64, i64, i64, i64, i32, vp]),
+    "rdmi_gather_unet_input": (i32, [vp, i64, vp, i64, i32, vp, i32, i64, vp, i32, vp]),
+    "rdmi_ddim_combine": (i32, [vp, i64, vp, i64, vp, i64, i64, i32, i32, f32, f32, f32, i64, i32, vp]),
+    "rdmi_snippet_average": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
     "rdmi_snippet_accumulate": (i32, [vp, i32, i32, i32, i32, i32, i32, i64, i32, i32, vp, vp]),
     "rdmi_snippet_finish": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
     "rdmi_minmax": (i32, [vp, i32, i64, vp, vp, vp]),

@@ -14,8 +14,10 @@ Semantics (b = batch of snippets, n = num_view frames per snippet):
 The reference supports only b = 1 per call (the cross-attention residual add
 fails for b > 1); this processor is correct for any b.
 
-Compute is f16 with f32 accumulation (librdmi); f32 inputs are cast to f16 on entry and the
-result cast back (the f32 kernel set is a later round), which the parity tests bound.
+Compute follows the input dtype: f32 inputs (the paper preset, run_video.py:444-449) run librdmi's
+f32 kernels (f32-input MFMA, exact f32 products); f16 / bf16 inputs run the f16 kernels with f32
+accumulation.  Layout changes of the 4-D (VAE) form and its residual add are librdmi transposes and
+the output GEMM's residual epilogue; PyTorch only allocates.
 """
 from __future__ import annotations
 
@@ -31,11 +33,11 @@ F16, F32 = torch.float16, torch.float32
 
 
 class _Packed:
-    def __init__(self, attn, dev):
+    def __init__(self, attn, dev, dtype):
         def lin(m):
             w = m.weight.detach().float().cpu()
             b = m.bias.detach().float().to(dev) if m.bias is not None else None
-            return K.pack_linear(w, dev), w.shape[1], b
+            return K.pack_linear(w, dev, dtype), w.shape[1], b
 
         self.q = lin(attn.to_q)
         self.k = lin(attn.to_k)
@@ -49,7 +51,7 @@ class _Packed:
             b = None
             if all(x is not None for x in bs):
                 b = torch.cat([x.detach().float() for x in bs]).to(dev)
-            self.self_qkv = (K.pack_linear(w, dev), w.shape[1], b)
+            self.self_qkv = (K.pack_linear(w, dev, dtype), w.shape[1], b)
         gn = attn.group_norm
         self.gn = None
         if gn is not None:
@@ -62,11 +64,15 @@ class CrossFrameAttnProcessor:
     def __init__(self):
         self._cache = weakref.WeakKeyDictionary()
 
-    def _packed(self, attn, dev) -> _Packed:
-        p = self._cache.get(attn)
+    def _packed(self, attn, dev, dtype) -> _Packed:
+        per = self._cache.get(attn)
+        if per is None:
+            per = {}
+            self._cache[attn] = per
+        p = per.get(dtype)
         if p is None:
-            p = _Packed(attn, dev)
-            self._cache[attn] = p
+            p = _Packed(attn, dev, dtype)
+            per[dtype] = p
         return p
 
     def __call__(self, attn, hidden_states: torch.Tensor, encoder_hidden_states: Optional[torch.Tensor] = None,
@@ -78,14 +84,15 @@ class CrossFrameAttnProcessor:
                 or getattr(attn, "norm_k", None) is not None or getattr(attn, "norm_cross", None):
             raise NotImplementedError("spatial_norm / qk-norm / norm_cross are not used on the RollingDepth path")
         in_dtype = hidden_states.dtype
+        cdt = F32 if in_dtype == F32 else F16
         dev = hidden_states.device
-        p = self._packed(attn, dev)
+        p = self._packed(attn, dev, cdt)
         residual = hidden_states
-        x = hidden_states.to(F16)
+        x = hidden_states.to(cdt)
         input_ndim = x.dim()
-        if input_ndim == 4:
+        if input_ndim == 4:  # [b, c, h, w] → token-major [b, hw, c]
             bsz, channel, height, width = x.shape
-            x = x.view(bsz, channel, height * width).transpose(1, 2)
+            x = K.transpose(x.reshape(bsz, channel, height * width))
         x = x.contiguous()
         if num_view is not None:  # "(b n) hw c -> b (n hw) c"
             x = x.view(x.shape[0] // num_view, num_view * x.shape[1], x.shape[2])
@@ -101,7 +108,7 @@ class CrossFrameAttnProcessor:
             inner = qkv.shape[-1] // 3
             q, k, v = qkv[..., :inner], qkv[..., inner:2 * inner], qkv[..., 2 * inner:]
         else:
-            ctx = x if encoder_hidden_states is None else encoder_hidden_states.to(dev, F16).contiguous()
+            ctx = x if encoder_hidden_states is None else encoder_hidden_states.to(dev, cdt).contiguous()
             q = K.gemm(flat, p.q[0], p.q[1], bias=p.q[2]).view(B, S, -1)
             cb, L, cd = ctx.shape
             k = K.gemm(ctx.view(cb * L, cd), p.k[0], p.k[1], bias=p.k[2]).view(cb, L, -1)
@@ -123,18 +130,19 @@ class CrossFrameAttnProcessor:
             vv = v if v.shape[0] == B else v.expand(B, -1, -1).contiguous()
             o = K.attention_1head(q, kk, vv, 1.0 / math.sqrt(D))
         res_tok = None
-        if attn.residual_connection and input_ndim == 3 and num_view is None:
-            res_tok = residual.to(F16).reshape(B * S, C).contiguous()
+        if attn.residual_connection:  # the residual enters the output GEMM's epilogue, token-major
+            if input_ndim == 4:
+                res_tok = K.transpose(residual.to(cdt).reshape(bsz, channel, height * width)).view(B * S, C)
+            else:
+                res_tok = residual.to(cdt).reshape(B * S, C).contiguous()
         out = K.gemm(o.reshape(B * S, inner), p.o[0], p.o[1], bias=p.o[2], residual=res_tok)
         if num_view is not None:  # "b (n hw) c -> (b n) hw c"
             out = out.view(B * num_view, S // num_view, C)
         else:
             out = out.view(B, S, C)
-        if input_ndim == 4:
-            out = out.transpose(-1, -2).reshape(bsz, channel, height, width)
+        if input_ndim == 4:  # token-major → [b, c, h, w]
+            out = K.transpose(out).view(bsz, channel, height, width)
         out = out.to(in_dtype)
-        if attn.residual_connection and res_tok is None:
-            out = out + residual
         if attn.rescale_output_factor != 1.0:
             out = out / attn.rescale_output_factor
         return out

@@ -92,13 +92,14 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
       (void*)(p.v + (long)b * p.v_bs + head * 64), (short)0, (int)(((long)(p.Sk - 1) * p.v_ld + 64) * 2), 0x00020000);
 
   // Q as the B operand of Sᵀ = K·Qᵀ: lane holds Q[qi][16ks + 8hh + 0..7] · scale·log2(e)
+  // (the product Q·scale·log2 e is formed in f32 and rounded to f16 once)
   f16x8 qf[4];
-  const f16 qs = (f16)p.sl2;
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     f16x8 z = {};
-    qf[ks] = qi < p.Sq ? *(const f16x8*)(Q + (long)qi * p.q_ld + ks * 16 + hh * 8) : z;
-    qf[ks] *= qs;
+    const f16x8 qr = qi < p.Sq ? *(const f16x8*)(Q + (long)qi * p.q_ld + ks * 16 + hh * 8) : z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qf[ks][e] = (f16)((float)qr[e] * p.sl2);
   }
   // the 65th dimension: A = ones column (k index 0 of the lanes < 32), B = -m̃ (same slot)
   // -m̃ enters as the chain's initial accumulator (rows are lane-local in the swapped layout, so all
@@ -318,35 +319,37 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
 }
 
 // one thread per (token, head); D == 64, L ≤ 16
-__global__ __launch_bounds__(256) void attn_smallkv(const f16* __restrict__ q, const f16* __restrict__ k,
-                                                    const f16* __restrict__ v, f16* __restrict__ o, int H, int Sq,
+template <typename T>
+__global__ __launch_bounds__(256) void attn_smallkv(const T* __restrict__ q, const T* __restrict__ k,
+                                                    const T* __restrict__ v, T* __restrict__ o, int H, int Sq,
                                                     int L, long q_ld, long o_ld, long q_bs, long o_bs, long kv_bs,
                                                     float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  f16* kl = (f16*)smem;              // [L][H*64]
-  f16* vl = kl + L * H * 64;
+  T* kl = (T*)smem;              // [L][H*64]
+  T* vl = kl + L * H * 64;
   const int b = blockIdx.y;
   const int HD = H * 64;
-  for (int i = threadIdx.x; i < L * HD / 8; i += blockDim.x) {
-    ((f16x8*)kl)[i] = ((const f16x8*)(k + (long)b * kv_bs))[i];
-    ((f16x8*)vl)[i] = ((const f16x8*)(v + (long)b * kv_bs))[i];
+  for (int i = threadIdx.x; i < L * HD * (int)sizeof(T) / 16; i += blockDim.x) {
+    ((f32x4*)kl)[i] = ((const f32x4*)(k + (long)b * kv_bs))[i];
+    ((f32x4*)vl)[i] = ((const f32x4*)(v + (long)b * kv_bs))[i];
   }
   __syncthreads();
   long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (idx >= (long)Sq * H) return;
   int tok = (int)(idx / H), h = (int)(idx % H);
-  const f16* qr = q + (long)b * q_bs + (long)tok * q_ld + h * 64;
+  const T* qr = q + (long)b * q_bs + (long)tok * q_ld + h * 64;
   float qv[64];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    f16x8 t = *(const f16x8*)(qr + 8 * i);
+    float t[8];
+    ld8(qr + 8 * i, t);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) qv[8 * i + e] = (float)t[e];
+    for (int e = 0; e < 8; ++e) qv[8 * i + e] = t[e];
   }
   float sc[16];
   float mx = -INFINITY;
   for (int j = 0; j < L; ++j) {
-    const f16* kr = kl + j * HD + h * 64;
+    const T* kr = kl + j * HD + h * 64;
     float a = 0.f;
 #pragma unroll
     for (int d = 0; d < 64; ++d) a += qv[d] * (float)kr[d];
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(256) void attn_smallkv(const f16* __restrict__ q, c
   }
   float den = 0.f;
   for (int j = 0; j < L; ++j) {
-    sc[j] = __expf(sc[j] - mx);
+    sc[j] = sizeof(T) == 2 ? __expf(sc[j] - mx) : expf(sc[j] - mx);
     den += sc[j];
   }
   float inv = 1.f / den;
@@ -363,22 +366,23 @@ __global__ __launch_bounds__(256) void attn_smallkv(const f16* __restrict__ q, c
 #pragma unroll
   for (int d = 0; d < 64; ++d) acc[d] = 0.f;
   for (int j = 0; j < L; ++j) {
-    const f16* vr = vl + j * HD + h * 64;
+    const T* vr = vl + j * HD + h * 64;
     float w = sc[j] * inv;
 #pragma unroll
     for (int d = 0; d < 64; ++d) acc[d] += w * (float)vr[d];
   }
-  f16* orow = o + (long)b * o_bs + (long)tok * o_ld + h * 64;
+  T* orow = o + (long)b * o_bs + (long)tok * o_ld + h * 64;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    f16x8 t;
+    float t[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) t[e] = (f16)acc[8 * i + e];
-    *(f16x8*)(orow + 8 * i) = t;
+    for (int e = 0; e < 8; ++e) t[e] = acc[8 * i + e];
+    st8(orow + 8 * i, t);
   }
 }
 
-__global__ __launch_bounds__(256) void softmax_rows_k(const float* __restrict__ s, f16* __restrict__ pout, long cols,
+template <typename TO>
+__global__ __launch_bounds__(256) void softmax_rows_k(const float* __restrict__ s, TO* __restrict__ pout, long cols,
                                                       long p_ld, float scale) {
   const long row = blockIdx.x;
   const float* sr = s + row * cols;
@@ -391,15 +395,17 @@ __global__ __launch_bounds__(256) void softmax_rows_k(const float* __restrict__ 
   mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   __syncthreads();
   float sum = 0.f;
-  for (long c = threadIdx.x; c < cols; c += 256) sum += __expf((sr[c] - mx) * scale);
+  for (long c = threadIdx.x; c < cols; c += 256)
+    sum += sizeof(TO) == 2 ? __expf((sr[c] - mx) * scale) : expf((sr[c] - mx) * scale);
   sum = wave_sum(sum);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
   __syncthreads();
   sum = red[0] + red[1] + red[2] + red[3];
   const float inv = 1.f / sum;
-  f16* pr = pout + row * p_ld;
-  for (long c = threadIdx.x; c < cols; c += 256) pr[c] = (f16)(__expf((sr[c] - mx) * scale) * inv);
-  for (long c = cols + threadIdx.x; c < p_ld; c += 256) pr[c] = (f16)0.f;  // K padding of the PV GEMM
+  TO* pr = pout + row * p_ld;
+  for (long c = threadIdx.x; c < cols; c += 256)
+    pr[c] = (TO)((sizeof(TO) == 2 ? __expf((sr[c] - mx) * scale) : expf((sr[c] - mx) * scale)) * inv);
+  for (long c = cols + threadIdx.x; c < p_ld; c += 256) pr[c] = (TO)0.f;  // K padding of the PV GEMM
 }
 
 // Single-pass row softmax: the row (≤ 1024·NV floats) is read once into registers as float4s,
@@ -575,10 +581,13 @@ __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f
 
 extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk,
                                   int D, long q_ld, long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs,
-                                  long o_bs, float scale, void* stream) {
+                                  long o_bs, float scale, int dtype, void* stream) {
   RDMI_REQUIRE(q && k && v && o, RDMI_E_ARG, "attention_fwd: null pointer");
   RDMI_REQUIRE(D == 64, RDMI_E_UNSUPPORTED, "attention_fwd: head_dim %d unsupported (64 only)", D);
   RDMI_REQUIRE(B > 0 && H > 0 && Sq > 0 && Sk > 0, RDMI_E_ARG, "attention_fwd: bad sizes");
+  if (dtype == RDMI_F32)
+    return rdmi::attention_fwd_f32(q, k, v, o, B, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs, scale,
+                                   stream);
   RDMI_REQUIRE(q_ld % 8 == 0 && k_ld % 8 == 0 && v_ld % 8 == 0 && o_ld % 4 == 0 && (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) == 0,
                RDMI_E_ALIGN, "attention_fwd: strides/pointers must be 16-byte aligned");
   AttnP p{(const f16*)q, (const f16*)k, (const f16*)v, (f16*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs,
@@ -594,20 +603,30 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
 
 extern "C" int rdmi_attention_smallkv(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int L,
                                       int D, long q_ld, long o_ld, long q_bs, long o_bs, long kv_bs, float scale,
-                                      void* stream) {
+                                      int dtype, void* stream) {
   RDMI_REQUIRE(q && k && v && o, RDMI_E_ARG, "attention_smallkv: null pointer");
   RDMI_REQUIRE(D == 64 && L >= 1 && L <= 16, RDMI_E_UNSUPPORTED, "attention_smallkv: D=%d L=%d unsupported", D, L);
-  size_t lds = (size_t)2 * L * H * 64 * sizeof(f16);
+  const size_t esz = dtype == RDMI_F32 ? 4 : 2;
+  size_t lds = (size_t)2 * L * H * 64 * esz;
   RDMI_REQUIRE(lds <= 64 * 1024, RDMI_E_UNSUPPORTED, "attention_smallkv: K/V too large for LDS");
   dim3 g(rdmi::div_up((long)Sq * H, 256), B);
-  hipLaunchKernelGGL(attn_smallkv, g, dim3(256), lds, (hipStream_t)stream, (const f16*)q, (const f16*)k, (const f16*)v,
-                     (f16*)o, H, Sq, L, q_ld, o_ld, q_bs, o_bs, kv_bs, scale);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(attn_smallkv<float>, g, dim3(256), lds, (hipStream_t)stream, (const float*)q, (const float*)k,
+                       (const float*)v, (float*)o, H, Sq, L, q_ld, o_ld, q_bs, o_bs, kv_bs, scale);
+  else
+    hipLaunchKernelGGL(attn_smallkv<f16>, g, dim3(256), lds, (hipStream_t)stream, (const f16*)q, (const f16*)k,
+                       (const f16*)v, (f16*)o, H, Sq, L, q_ld, o_ld, q_bs, o_bs, kv_bs, scale);
   return rdmi::check_launch("attention_smallkv");
 }
 
-extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, void* stream) {
+extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, long p_ld, float scale, int p_dtype,
+                                 void* stream) {
   RDMI_REQUIRE(s && p && rows > 0 && cols > 0 && p_ld >= cols, RDMI_E_ARG, "softmax_rows: bad args");
   hipStream_t st = (hipStream_t)stream;
+  if (p_dtype == RDMI_F32) {
+    hipLaunchKernelGGL(softmax_rows_k<float>, dim3((unsigned)rows), dim3(256), 0, st, s, (float*)p, cols, p_ld, scale);
+    return rdmi::check_launch("softmax_rows");
+  }
   const bool vec = cols % 4 == 0 && p_ld % 4 == 0 && ((uintptr_t)s & 15) == 0 && ((uintptr_t)p & 7) == 0;
   const long nv = (cols / 4 + 255) / 256;  // float4s per thread
   if (vec && nv <= 4)
@@ -615,7 +634,7 @@ extern "C" int rdmi_softmax_rows(const float* s, void* p, long rows, long cols, 
   else if (vec && nv <= 16)
     hipLaunchKernelGGL(softmax_rows_reg_k<16>, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
   else
-    hipLaunchKernelGGL(softmax_rows_k, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
+    hipLaunchKernelGGL(softmax_rows_k<f16>, dim3((unsigned)rows), dim3(256), 0, st, s, (f16*)p, cols, p_ld, scale);
   return rdmi::check_launch("softmax_rows");
 }
 

@@ -1,0 +1,214 @@
+// f32 cross-frame flash attention (the paper preset's fp32 SDPA, attention_processor.py:2251-2253,
+// behind rdmi_attention_fwd with dtype RDMI_F32).  head_dim 64, non-causal, no mask.
+//
+// gfx950 runs f32 matrix products only on v_mfma_f32_16x16x4_f32 (exact f32, 1/16 of the f16 rate),
+// so this kernel is MFMA-bound by a wide margin and its design goal is to keep the matrix pipe fed:
+//   * workgroup = 8 waves × 32 queries (two 16-query fragments per wave) of one (snippet, head); K/V
+//     tiles of 64 keys are staged in LDS (double-buffered: the next tile's global loads are in flight
+//     in registers while the current tile's MFMAs run) and shared by the 256 queries;
+//   * Sᵀ = K·Qᵀ: lane l owns query l & 15 of a fragment and keys 4(l >> 4) + r (r = 0..3) of each
+//     16-key fragment, so the online-softmax row max / sum are lane-local plus two cross-quarter
+//     shuffles; Q (prescaled by scale·log2 e in f32) stays in registers; lane quarter q supplies
+//     head dims 16q + s at MFMA step s for both operands (four 16-B K reads per fragment);
+//   * Oᵀ = Vᵀ·Pᵀ re-uses the Sᵀ accumulator as the B operand unchanged (its keys are already in the
+//     lane-quarter k order) and reads V[key][d] from LDS (row stride 68 floats: the four lane
+//     quarters' rows land on disjoint bank groups); Oᵀ has the query on the lane too, so the
+//     per-query rescale exp2(m_old − m_new) is lane-local.
+// Softmax in exp2 domain, f32 throughout; row sums kept per lane and combined across the lane
+// quarters once at the end (the rescale factor is common to the quarters).
+#include "common.h"
+
+namespace {
+
+struct AttnF32P {
+  const float* q; const float* k; const float* v; float* o;
+  int H, Sq, Sk;
+  long q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs;
+  float sl2;  // scale · log2(e)
+};
+
+constexpr int NWF = 8;          // waves per workgroup
+constexpr int QF = 2;           // 16-query fragments per wave
+constexpr int QBF = NWF * QF * 16;  // 256 queries per workgroup
+constexpr int KT = 64;          // keys per tile
+constexpr int KFR = KT / 16;    // key fragments per tile
+constexpr int KROW = 64;        // K tile row: 64 floats (256 B), 16-B chunks XOR-swizzled by (row & 15)
+constexpr int VROW = 68;        // V tile row stride (floats)
+constexpr int KTILE = KT * KROW, VTILE = KT * VROW;
+constexpr int LPT = (KT * 64 / 4) / (64 * NWF);  // f32x4 loads per thread per tile per tensor (2)
+
+__global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32(AttnF32P p) {
+  __shared__ __attribute__((aligned(16))) float kl[2][KTILE];
+  __shared__ __attribute__((aligned(16))) float vl[2][VTILE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, qq = lane >> 4;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QBF + wid * QF * 16;
+  const float* Q = p.q + (long)b * p.q_bs + head * 64;
+  const float* Kg = p.k + (long)b * p.k_bs + head * 64;
+  const float* Vg = p.v + (long)b * p.v_bs + head * 64;
+
+  // Q fragments: lane holds Q[q0 + 16f + fr][16qq .. 16qq + 15] · scale·log2(e)
+  float qv[QF][16];
+#pragma unroll
+  for (int f = 0; f < QF; ++f) {
+    const int qi = q0 + 16 * f + fr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f32x4 t = qi < p.Sq ? *(const f32x4*)(Q + (long)qi * p.q_ld + 16 * qq + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qv[f][4 * c + e] = t[e] * p.sl2;
+    }
+  }
+
+  // tile loads: thread handles f32x4 chunk i*512 + tid of the 64×64 tile (row = idx >> 4, chunk = idx & 15)
+  f32x4 kr[LPT], vr[LPT];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = i * 64 * NWF + tid;
+      const int row = idx >> 4, ch = idx & 15;
+      const int key = kt * KT + row;
+      const bool ok = key < p.Sk;
+      kr[i] = ok ? *(const f32x4*)(Kg + (long)key * p.k_ld + ch * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      vr[i] = ok ? *(const f32x4*)(Vg + (long)key * p.v_ld + ch * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto lstore = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = i * 64 * NWF + tid;
+      const int row = idx >> 4, ch = idx & 15;
+      *(f32x4*)(&kl[slot][row * KROW + ((ch ^ (row & 15)) << 2)]) = kr[i];
+      *(f32x4*)(&vl[slot][row * VROW + ch * 4]) = vr[i];
+    }
+  };
+
+  f32x4 o[QF][4];  // Oᵀ fragments: d = 16e + 4qq + r, query = 16f + fr
+  float m[QF], l[QF];
+#pragma unroll
+  for (int f = 0; f < QF; ++f) {
+    m[f] = -INFINITY;
+    l[f] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[f][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int nkt = (p.Sk + KT - 1) / KT;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int slot = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);  // next tile's global loads in flight under this tile's MFMAs
+    const float* kb = kl[slot];
+    const float* vb = vl[slot];
+    // Sᵀ = K·Qᵀ
+    f32x4 s[QF][KFR];
+#pragma unroll
+    for (int g = 0; g < KFR; ++g) {
+      const int row = 16 * g + fr;
+      float kf[16];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f32x4 t = *(const f32x4*)(kb + row * KROW + (((4 * qq + c) ^ (row & 15)) << 2));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kf[4 * c + e] = t[e];
+      }
+#pragma unroll
+      for (int f = 0; f < QF; ++f) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 16; ++st) a = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[st], qv[f][st], a, 0, 0, 0);
+        s[f][g] = a;
+      }
+    }
+    // keys past Sk (last tile only)
+    if ((kt + 1) * KT > p.Sk) {
+#pragma unroll
+      for (int g = 0; g < KFR; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * KT + 16 * g + 4 * qq + r >= p.Sk)
+#pragma unroll
+            for (int f = 0; f < QF; ++f) s[f][g][r] = -INFINITY;
+    }
+    // online softmax (exp2 domain)
+#pragma unroll
+    for (int f = 0; f < QF; ++f) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < KFR; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[f][g][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[f], mx);
+      const float alpha = exp2f(m[f] - mn);
+      m[f] = mn;
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < KFR; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = exp2f(s[f][g][r] - mn);
+          s[f][g][r] = pv;
+          sum += pv;
+        }
+      l[f] = l[f] * alpha + sum;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[f][e] *= alpha;
+    }
+    // Oᵀ += Vᵀ·Pᵀ: step r of key fragment g uses key 16g + 4qq + r on both operands
+#pragma unroll
+    for (int g = 0; g < KFR; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float* vrow = vb + (16 * g + 4 * qq + r) * VROW + fr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float va = vrow[16 * e];
+#pragma unroll
+          for (int f = 0; f < QF; ++f) o[f][e] = __builtin_amdgcn_mfma_f32_16x16x4f32(va, s[f][g][r], o[f][e], 0, 0, 0);
+        }
+      }
+    __syncthreads();  // every wave is done with the other slot (read in tile kt-1)
+    if (kt + 1 < nkt) {
+      lstore(slot ^ 1);
+      __syncthreads();
+    }
+  }
+  // finish: l summed over the lane quarters, O / l, store O[q][d..d+3]
+#pragma unroll
+  for (int f = 0; f < QF; ++f) {
+    float lt = l[f];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.0f / lt;
+    const int qi = q0 + 16 * f + fr;
+    if (qi < p.Sq) {
+      float* orow = p.o + (long)b * p.o_bs + (long)qi * p.o_ld + head * 64;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *(f32x4*)(orow + 16 * e + 4 * qq) = o[f][e] * inv;
+    }
+  }
+}
+
+}  // namespace
+
+namespace rdmi {
+
+int attention_fwd_f32(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, long q_ld,
+                      long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs, long o_bs, float scale,
+                      void* stream) {
+  RDMI_REQUIRE(q_ld % 4 == 0 && k_ld % 4 == 0 && v_ld % 4 == 0 && o_ld % 4 == 0 &&
+                   ((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) == 0),
+               RDMI_E_ALIGN, "attention_fwd f32: strides/pointers must be 16-byte aligned");
+  AttnF32P p{(const float*)q, (const float*)k, (const float*)v, (float*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld,
+             q_bs, k_bs, v_bs, o_bs, scale * 1.4426950408889634f};
+  dim3 g(rdmi::div_up(Sq, QBF), H, B);
+  hipLaunchKernelGGL(attn_fwd_f32, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
+  return rdmi::check_launch("attention_fwd f32");
+}
+
+}  // namespace rdmi

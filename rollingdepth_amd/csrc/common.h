@@ -27,7 +27,46 @@ void set_error(const char* fmt, ...);
 // Check a launch; returns 0 or the HIP error code (message recorded).
 int check_launch(const char* what);
 
+// f32 engines behind rdmi_gemm / rdmi_conv2d (gemm_f32.hip), selected by args->dtype == RDMI_F32
+int gemm_f32(const rdmi_gemm_args* a, void* stream);
+int conv2d_f32(const rdmi_conv_args* a, void* stream);
+// f32 flash attention behind rdmi_attention_fwd (attention_f32.hip)
+int attention_fwd_f32(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, long q_ld,
+                      long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs, long o_bs, float scale,
+                      void* stream);
+
 inline int div_up(long a, long b) { return (int)((a + b - 1) / b); }
+
+// XCD-aware remap (T1): dispatch id d runs on XCD d % 8; give each XCD a contiguous range of
+// logical tiles so the n-tiles sharing one A row-panel share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int total) {
+  if (total < 8) return bid;
+  const int xcd = bid & 7, q = total >> 3, r = total & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// logical tile → (m-tile, n-tile): groups of G m-tiles sweep all n-tiles with m fastest, so the
+// tiles an XCD runs together share G A-panels and a few B-panels (L2 reuse in both operands)
+__device__ __forceinline__ void tile_mn(int logical, int nbx, int nby, int G, int& mt, int& nt) {
+  if (G <= 1) {
+    mt = logical / nbx;
+    nt = logical % nbx;
+    return;
+  }
+  const int per = G * nbx;
+  const int g = logical / per;
+  const int first = g * G;
+  const int gs = min(G, nby - first);
+  const int r = logical - g * per;
+  mt = first + r % gs;
+  nt = r / gs;
+}
+
+// vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_only() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+}
 
 }  // namespace rdmi
 
@@ -78,3 +117,32 @@ __device__ __forceinline__ float wave_min(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
   return v;
 }
+
+// 8-element vector load / store in either storage dtype (f16: one 16-B access; f32: two), values in
+// f32 registers.  Lets one kernel template serve the f16 path and the paper preset's f32 path.
+__device__ __forceinline__ void ld8(const f16* p, float (&v)[8]) {
+  const f16x8 x = *(const f16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+}
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = a[e];
+    v[4 + e] = b[e];
+  }
+}
+__device__ __forceinline__ void st8(f16* p, const float (&v)[8]) {
+  f16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (f16)v[e];
+  *(f16x8*)p = o;
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+// the value a store of f in dtype T reads back as (the rounding the next op sees)
+__device__ __forceinline__ float rt(f16*, float f) { return (float)(f16)f; }
+__device__ __forceinline__ float rt(float*, float f) { return f; }

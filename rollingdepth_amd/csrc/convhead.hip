@@ -18,7 +18,8 @@ namespace {
 constexpr int HT = 256;  // threads per workgroup
 
 // pass 1: x [B][HW][C] f16, mr [B*G][2] {mean, rstd}, gamma/beta [C] f32, w [9][C] f32 → d [9][B*HW]
-__global__ __launch_bounds__(HT) void head_taps(const f16* __restrict__ x, long HW, int C, int G,
+template <typename T>
+__global__ __launch_bounds__(HT) void head_taps(const T* __restrict__ x, long HW, int C, int G,
                                                 const float* __restrict__ mr, const float* __restrict__ gamma,
                                                 const float* __restrict__ beta, const float* __restrict__ w,
                                                 int silu, float* __restrict__ d, long P) {
@@ -38,17 +39,18 @@ __global__ __launch_bounds__(HT) void head_taps(const f16* __restrict__ x, long 
   __syncthreads();
   const long p = (long)blockIdx.x * HT + threadIdx.x;
   if (p >= HW) return;
-  const f16* xp = x + ((long)b * HW + p) * C;
+  const T* xp = x + ((long)b * HW + p) * C;
   float acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = 0.f;
   for (int c0 = 0; c0 < C; c0 += 8) {
-    const f16x8 v = *(const f16x8*)(xp + c0);
+    float v[8];
+    ld8(xp + c0, v);
     float y[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float f = fmaf((float)v[e], sc[c0 + e], sh[c0 + e]);
-      y[e] = silu ? silu_f(f) : f;
+      const float f = fmaf(v[e], sc[c0 + e], sh[c0 + e]);
+      y[e] = silu ? (sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f))) : f;
     }
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -64,8 +66,8 @@ __global__ __launch_bounds__(HT) void head_taps(const f16* __restrict__ x, long 
 // normalising and weighting 8 channels, so one wave load instruction reads 64/LPP whole pixel
 // rows (the per-thread form above reads 64 rows 2·C bytes apart per instruction); the 9 tap sums
 // are reduced across the LPP lanes in a fixed butterfly and written pixel-major, d[p][9].
-template <int LPP>
-__global__ __launch_bounds__(HT) void head_taps_v(const f16* __restrict__ x, long HW, int G,
+template <typename T, int LPP>
+__global__ __launch_bounds__(HT) void head_taps_v(const T* __restrict__ x, long HW, int G,
                                                   const float* __restrict__ mr, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, const float* __restrict__ w,
                                                   int silu, float* __restrict__ d, long P, int ppb) {
@@ -87,14 +89,15 @@ __global__ __launch_bounds__(HT) void head_taps_v(const f16* __restrict__ x, lon
   const long pbeg = (long)blockIdx.x * ppb;
   const long pend = pbeg + ppb < HW ? pbeg + ppb : HW;
   for (long p = pbeg + threadIdx.x / LPP; p < pend; p += HT / LPP) {
-    const f16x8 v = *(const f16x8*)(x + ((long)b * HW + p) * C + c0);
+    float v[8];
+    ld8(x + ((long)b * HW + p) * C + c0, v);
     float acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t] = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float f = fmaf((float)v[e], sc[e], sh[e]);
-      if (silu) f = silu_f(f);
+      float f = fmaf(v[e], sc[e], sh[e]);
+      if (silu) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[t] = fmaf(f, wt[t][e], acc[t]);
     }
@@ -110,8 +113,9 @@ __global__ __launch_bounds__(HT) void head_taps_v(const f16* __restrict__ x, lon
 }
 
 // pass 2 for the pixel-major taps: out[q] = bias + Σ_{dy,dx} d[q + (dy-1)·W + dx-1][3dy+dx]
+template <typename T>
 __global__ __launch_bounds__(HT) void head_gather_v(const float* __restrict__ d, int H, int W, long P, float bias,
-                                                    f16* __restrict__ out) {
+                                                    T* __restrict__ out) {
   const long q = (long)blockIdx.x * HT + threadIdx.x;
   if (q >= P) return;
   const long HW = (long)H * W;
@@ -130,12 +134,13 @@ __global__ __launch_bounds__(HT) void head_gather_v(const float* __restrict__ d,
       s += d[(b * HW + (long)hh * W + ww) * 9 + 3 * dy + dx];
     }
   }
-  out[q] = (f16)s;
+  out[q] = (T)s;
 }
 
 // pass 2: out[b][h][w] = bias + Σ_{dy,dx} d[3dy+dx][b][h+dy-1][w+dx-1] (zero outside the image)
+template <typename T>
 __global__ __launch_bounds__(HT) void head_gather(const float* __restrict__ d, int H, int W, long P, float bias,
-                                                  f16* __restrict__ out) {
+                                                  T* __restrict__ out) {
   const long q = (long)blockIdx.x * HT + threadIdx.x;
   if (q >= P) return;
   const long HW = (long)H * W;
@@ -154,30 +159,21 @@ __global__ __launch_bounds__(HT) void head_gather(const float* __restrict__ d, i
       s += d[(3 * dy + dx) * P + b * HW + (long)hh * W + ww];
     }
   }
-  out[q] = (f16)s;
+  out[q] = (T)s;
 }
 
-}  // namespace
-
-extern "C" long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W) { return 9L * B * H * W; }
-
-extern "C" int rdmi_conv3x3_to1_gn(const void* x, int B, int H, int W, int C, int G, const float* mean_rstd,
-                                   const float* gamma, const float* beta, int silu, const float* w, float bias,
-                                   void* y, float* workspace, void* stream) {
-  RDMI_REQUIRE(x && mean_rstd && gamma && beta && w && y && workspace, RDMI_E_ARG, "conv3x3_to1_gn: null pointer");
-  RDMI_REQUIRE(B > 0 && H > 0 && W > 0 && C % 8 == 0 && C > 0 && C <= 1024 && G > 0 && C % G == 0, RDMI_E_ARG,
-               "conv3x3_to1_gn: bad sizes B=%d H=%d W=%d C=%d G=%d", B, H, W, C, G);
-  RDMI_REQUIRE(((uintptr_t)x & 15) == 0, RDMI_E_ALIGN, "conv3x3_to1_gn: x not 16-byte aligned");
+template <typename T>
+int head_launch(const void* x, int B, int H, int W, int C, int G, const float* mean_rstd, const float* gamma,
+                const float* beta, int silu, const float* w, float bias, void* y, float* workspace, hipStream_t s) {
   const long HW = (long)H * W, P = (long)B * HW;
-  hipStream_t s = (hipStream_t)stream;
   const int lpp = C / 8;
   if (lpp == 16 || lpp == 32 || lpp == 64 || lpp == 8 || lpp == 4 || lpp == 2 || lpp == 1) {
     constexpr int PPB = 1024;  // pixels per workgroup
     dim3 g(rdmi::div_up(HW, PPB), B);
-#define RDMI_HEAD(L)                                                                                        \
-  case L:                                                                                                   \
-    hipLaunchKernelGGL(head_taps_v<L>, g, dim3(HT), 0, s, (const f16*)x, HW, G, mean_rstd, gamma, beta, w, \
-                       silu, workspace, P, PPB);                                                            \
+#define RDMI_HEAD(L)                                                                                             \
+  case L:                                                                                                        \
+    hipLaunchKernelGGL((head_taps_v<T, L>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma, beta, w,   \
+                       silu, workspace, P, PPB);                                                                 \
     break;
     switch (lpp) {
       RDMI_HEAD(1) RDMI_HEAD(2) RDMI_HEAD(4) RDMI_HEAD(8) RDMI_HEAD(16) RDMI_HEAD(32) RDMI_HEAD(64)
@@ -186,14 +182,30 @@ extern "C" int rdmi_conv3x3_to1_gn(const void* x, int B, int H, int W, int C, in
 #undef RDMI_HEAD
     int rc = rdmi::check_launch("conv3x3_to1_gn taps");
     if (rc) return rc;
-    hipLaunchKernelGGL(head_gather_v, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (f16*)y);
+    hipLaunchKernelGGL(head_gather_v<T>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (T*)y);
     return rdmi::check_launch("conv3x3_to1_gn gather");
   }
   const size_t lds = (size_t)11 * C * sizeof(float);
-  hipLaunchKernelGGL(head_taps, dim3(rdmi::div_up(HW, HT), B), dim3(HT), lds, s, (const f16*)x, HW, C, G, mean_rstd,
+  hipLaunchKernelGGL(head_taps<T>, dim3(rdmi::div_up(HW, HT), B), dim3(HT), lds, s, (const T*)x, HW, C, G, mean_rstd,
                      gamma, beta, w, silu, workspace, P);
   int rc = rdmi::check_launch("conv3x3_to1_gn taps");
   if (rc) return rc;
-  hipLaunchKernelGGL(head_gather, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (f16*)y);
+  hipLaunchKernelGGL(head_gather<T>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (T*)y);
   return rdmi::check_launch("conv3x3_to1_gn gather");
+}
+
+}  // namespace
+
+extern "C" long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W) { return 9L * B * H * W; }
+
+extern "C" int rdmi_conv3x3_to1_gn(const void* x, int dtype, int B, int H, int W, int C, int G, const float* mean_rstd,
+                                   const float* gamma, const float* beta, int silu, const float* w, float bias,
+                                   void* y, float* workspace, void* stream) {
+  RDMI_REQUIRE(x && mean_rstd && gamma && beta && w && y && workspace, RDMI_E_ARG, "conv3x3_to1_gn: null pointer");
+  RDMI_REQUIRE(B > 0 && H > 0 && W > 0 && C % 8 == 0 && C > 0 && C <= 1024 && G > 0 && C % G == 0, RDMI_E_ARG,
+               "conv3x3_to1_gn: bad sizes B=%d H=%d W=%d C=%d G=%d", B, H, W, C, G);
+  RDMI_REQUIRE(((uintptr_t)x & 15) == 0, RDMI_E_ALIGN, "conv3x3_to1_gn: x not 16-byte aligned");
+  if (dtype == RDMI_F32)
+    return head_launch<float>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, (hipStream_t)stream);
+  return head_launch<f16>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, (hipStream_t)stream);
 }

@@ -11,7 +11,8 @@ inline unsigned grid_for(long n, int per_block = 256) {
   return (unsigned)g;
 }
 
-__global__ void nchw_to_nhwc_k(const void* __restrict__ x, int x_f32, f16* __restrict__ y, int C, long HW, int Cpad,
+template <typename TO>
+__global__ void nchw_to_nhwc_k(const void* __restrict__ x, int x_f32, TO* __restrict__ y, int C, long HW, int Cpad,
                                long n, float scale, long bstride, long cstride) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     long pix = i / Cpad;
@@ -23,11 +24,12 @@ __global__ void nchw_to_nhwc_k(const void* __restrict__ x, int x_f32, f16* __res
       v = x_f32 ? ((const float*)x)[src] : (float)((const f16*)x)[src];
       v *= scale;
     }
-    y[i] = (f16)v;
+    y[i] = (TO)v;
   }
 }
 
-__global__ void nhwc_to_nchw_k(const f16* __restrict__ x, long ld, float* __restrict__ y, int C, long HW, long n,
+template <typename T>
+__global__ void nhwc_to_nchw_k(const T* __restrict__ x, long ld, float* __restrict__ y, int C, long HW, long n,
                                float scale, float shift) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     long bc = i / HW, p = i - bc * HW;
@@ -37,21 +39,21 @@ __global__ void nhwc_to_nchw_k(const f16* __restrict__ x, long ld, float* __rest
   }
 }
 
-__global__ void concat_k(const f16* __restrict__ a, int Ca, const f16* __restrict__ b, int Cb, f16* __restrict__ y,
+// Ca, Cb in 16-B vectors (8 halves or 4 floats)
+__global__ void concat_k(const f32x4* __restrict__ a, int AV, const f32x4* __restrict__ b, int BVv, f32x4* __restrict__ y,
                          long P) {
-  const int CV = (Ca + Cb) >> 3, AV = Ca >> 3, BVv = Cb >> 3;
+  const int CV = AV + BVv;
   long n = P * CV;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     long p = i / CV;
     int cv = (int)(i - p * CV);
-    f16x8 v = cv < AV ? ((const f16x8*)a)[p * AV + cv] : ((const f16x8*)b)[p * BVv + (cv - AV)];
-    ((f16x8*)y)[i] = v;
+    y[i] = cv < AV ? a[p * AV + cv] : b[p * BVv + (cv - AV)];
   }
 }
 
 // nearest resize, PyTorch's index rule for an explicit output size: src = min(floor(dst·(in/out)), in−1)
 // with the scale in f32 (F.interpolate(mode="nearest", size=...), as Upsample2D uses it)
-__global__ void resize_nearest_k(const f16* __restrict__ x, int H, int W, int CV, f16* __restrict__ y, int Ho, int Wo,
+__global__ void resize_nearest_k(const f32x4* __restrict__ x, int H, int W, int CV, f32x4* __restrict__ y, int Ho, int Wo,
                                  long n) {
   const float sy = (float)H / (float)Ho, sx = (float)W / (float)Wo;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -62,13 +64,14 @@ __global__ void resize_nearest_k(const f16* __restrict__ x, int H, int W, int CV
     const int yo = (int)(r % Ho);
     const long b = r / Ho;
     const int yi = min((int)floorf((float)yo * sy), H - 1), xi = min((int)floorf((float)xo * sx), W - 1);
-    ((f16x8*)y)[i] = ((const f16x8*)x)[((b * H + yi) * W + xi) * CV + cv];
+    y[i] = x[((b * H + yi) * W + xi) * CV + cv];
   }
 }
 
-__global__ void transpose_k(const f16* __restrict__ src, f16* __restrict__ dst, long rows, long cols, long sld,
+template <typename T>
+__global__ void transpose_k(const T* __restrict__ src, T* __restrict__ dst, long rows, long cols, long sld,
                             long dld) {
-  __shared__ f16 tile[64][65];
+  __shared__ T tile[64][65];
   const int b = blockIdx.z;
   const long r0 = blockIdx.y * 64L, c0 = blockIdx.x * 64L;
   src += (long)b * rows * sld;
@@ -85,28 +88,30 @@ __global__ void transpose_k(const f16* __restrict__ src, f16* __restrict__ dst, 
 }
 
 // out [count][HW][8]: rgb latent channels 0..3, depth latent 4..7
-__global__ void gather_unet_input_k(const f16* __restrict__ rgb, long rgb_ld, const f16* __restrict__ depth,
+template <typename T>
+__global__ void gather_unet_input_k(const T* __restrict__ rgb, long rgb_ld, const T* __restrict__ depth,
                                     long depth_ld, int bcast, const int* __restrict__ fidx, int count, long HW,
-                                    f16* __restrict__ out) {
+                                    T* __restrict__ out) {
   long n = (long)count * HW;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     int s = (int)(i / HW);
     long p = i - (long)s * HW;
     int f = fidx[s];
-    const f16* r = rgb + (long)f * rgb_ld + p * 8;
-    const f16* d = depth + (bcast ? 0 : (long)f * depth_ld) + p * 8;
-    f16x8 v;
+    const T* r = rgb + (long)f * rgb_ld + p * 8;
+    const T* d = depth + (bcast ? 0 : (long)f * depth_ld) + p * 8;
+    float v[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[e] = r[e];
-      v[4 + e] = d[e];
+      v[e] = (float)r[e];
+      v[4 + e] = (float)d[e];
     }
-    ((f16x8*)out)[i] = v;
+    st8(out + i * 8, v);
   }
 }
 
-__global__ void ddim_combine_k(const f16* __restrict__ x, long ldx, const f16* __restrict__ e, long lde,
-                               f16* __restrict__ y, long ldy, long P, int C, int Cpad, float ca, float cb, float sc,
+template <typename T>
+__global__ void ddim_combine_k(const T* __restrict__ x, long ldx, const T* __restrict__ e, long lde,
+                               T* __restrict__ y, long ldy, long P, int C, int Cpad, float ca, float cb, float sc,
                                long e_period) {
   long n = P * Cpad;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -115,14 +120,15 @@ __global__ void ddim_combine_k(const f16* __restrict__ x, long ldx, const f16* _
     long pe = e_period > 0 ? p % e_period : p;
     float v = 0.f;
     if (c < C) v = (ca * (float)x[p * ldx + c] + cb * (float)e[pe * lde + c]) * sc;
-    y[p * ldy + c] = (f16)v;
+    y[p * ldy + c] = (T)v;
   }
 }
 
 // refine (rollingdepth_pipeline.py:586-629): new[f] = mean over the snippets s covering f
 // (s = f - j*stride, slot j) of pred[s][j]; accumulated in f32 in snippet order.
-__global__ void snippet_average_k(const f16* __restrict__ src, int n, int w, int stride, long P, int C, int ld,
-                                  f16* __restrict__ out) {
+template <typename T>
+__global__ void snippet_average_k(const T* __restrict__ src, int n, int w, int stride, long P, int C, int ld,
+                                  T* __restrict__ out) {
   const int f = blockIdx.y;
   const long tot = P * ld;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
@@ -139,7 +145,7 @@ __global__ void snippet_average_k(const f16* __restrict__ src, int n, int w, int
       }
       v = cnt ? s / (float)cnt : 0.f;
     }
-    out[(long)f * tot + i] = (f16)v;
+    out[(long)f * tot + i] = (T)v;
   }
 }
 
@@ -253,66 +259,92 @@ __global__ void renorm_k(float* __restrict__ x, long n, const float* __restrict_
 
 }  // namespace
 
-extern "C" int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int B, int C, int H, int W, int Cpad, float scale,
-                                 long x_bstride, long x_cstride, void* stream) {
+extern "C" int rdmi_nchw_to_nhwc(const void* x, int x_f32, void* y, int y_dtype, int B, int C, int H, int W, int Cpad,
+                                 float scale, long x_bstride, long x_cstride, void* stream) {
   RDMI_REQUIRE(x && y && Cpad >= C, RDMI_E_ARG, "nchw_to_nhwc: bad args");
   long n = (long)B * H * W * Cpad;
-  hipLaunchKernelGGL(nchw_to_nhwc_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, x_f32, (f16*)y, C,
-                     (long)H * W, Cpad, n, scale, x_bstride, x_cstride);
+  if (y_dtype == RDMI_F32)
+    hipLaunchKernelGGL(nchw_to_nhwc_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, x_f32,
+                       (float*)y, C, (long)H * W, Cpad, n, scale, x_bstride, x_cstride);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_k<f16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, x_f32, (f16*)y,
+                       C, (long)H * W, Cpad, n, scale, x_bstride, x_cstride);
   return rdmi::check_launch("nchw_to_nhwc");
 }
 
-extern "C" int rdmi_nhwc_to_nchw_f32(const void* x, long ld, float* y, int B, int C, int H, int W, float scale,
-                                     float shift, void* stream) {
+extern "C" int rdmi_nhwc_to_nchw_f32(const void* x, int dtype, long ld, float* y, int B, int C, int H, int W,
+                                     float scale, float shift, void* stream) {
   RDMI_REQUIRE(x && y && ld >= C, RDMI_E_ARG, "nhwc_to_nchw: bad args");
   long n = (long)B * C * H * W;
-  hipLaunchKernelGGL(nhwc_to_nchw_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld, y, C,
-                     (long)H * W, n, scale, shift);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(nhwc_to_nchw_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const float*)x, ld,
+                       y, C, (long)H * W, n, scale, shift);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_k<f16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld, y,
+                       C, (long)H * W, n, scale, shift);
   return rdmi::check_launch("nhwc_to_nchw");
 }
 
-extern "C" int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, void* stream) {
-  RDMI_REQUIRE(a && b && y && Ca % 8 == 0 && Cb % 8 == 0, RDMI_E_ALIGN, "concat: channels must be multiples of 8");
-  long n = P * ((Ca + Cb) / 8);
-  hipLaunchKernelGGL(concat_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)a, Ca, (const f16*)b,
-                     Cb, (f16*)y, P);
+extern "C" int rdmi_concat_channels(const void* a, int Ca, const void* b, int Cb, void* y, long P, int dtype,
+                                    void* stream) {
+  const int per = dtype == RDMI_F32 ? 4 : 8;  // elements per 16-B vector
+  RDMI_REQUIRE(a && b && y && Ca % per == 0 && Cb % per == 0, RDMI_E_ALIGN,
+               "concat: channels must be multiples of %d", per);
+  long n = P * ((Ca + Cb) / per);
+  hipLaunchKernelGGL(concat_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f32x4*)a, Ca / per,
+                     (const f32x4*)b, Cb / per, (f32x4*)y, P);
   return rdmi::check_launch("concat");
 }
 
-extern "C" int rdmi_resize_nearest(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo, void* stream) {
+extern "C" int rdmi_resize_nearest(const void* x, int B, int H, int W, int C, void* y, int Ho, int Wo, int dtype,
+                                   void* stream) {
   RDMI_REQUIRE(x && y && B > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0, RDMI_E_ARG, "resize_nearest: bad args");
-  RDMI_REQUIRE(C % 8 == 0, RDMI_E_ALIGN, "resize_nearest: C (%d) must be a multiple of 8", C);
-  const long n = (long)B * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(resize_nearest_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, H, W, C / 8,
-                     (f16*)y, Ho, Wo, n);
+  const int per = dtype == RDMI_F32 ? 4 : 8;
+  RDMI_REQUIRE(C % per == 0, RDMI_E_ALIGN, "resize_nearest: C (%d) must be a multiple of %d", C, per);
+  const long n = (long)B * Ho * Wo * (C / per);
+  hipLaunchKernelGGL(resize_nearest_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f32x4*)x, H, W,
+                     C / per, (f32x4*)y, Ho, Wo, n);
   return rdmi::check_launch("resize_nearest");
 }
 
 extern "C" int rdmi_transpose(const void* src, void* dst, int batch, long rows, long cols, long src_ld, long dst_ld,
-                              void* stream) {
+                              int dtype, void* stream) {
   RDMI_REQUIRE(src && dst && rows > 0 && cols > 0, RDMI_E_ARG, "transpose: bad args");
   dim3 g(rdmi::div_up(cols, 64), rdmi::div_up(rows, 64), batch);
-  hipLaunchKernelGGL(transpose_k, g, dim3(64, 4), 0, (hipStream_t)stream, (const f16*)src, (f16*)dst, rows, cols,
-                     src_ld, dst_ld);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(transpose_k<float>, g, dim3(64, 4), 0, (hipStream_t)stream, (const float*)src, (float*)dst, rows,
+                       cols, src_ld, dst_ld);
+  else
+    hipLaunchKernelGGL(transpose_k<f16>, g, dim3(64, 4), 0, (hipStream_t)stream, (const f16*)src, (f16*)dst, rows, cols,
+                       src_ld, dst_ld);
   return rdmi::check_launch("transpose");
 }
 
 extern "C" int rdmi_gather_unet_input(const void* rgb, long rgb_frame_ld, const void* depth, long depth_frame_ld,
-                                      int depth_bcast, const int* frame_idx, int count, long HW, void* out,
+                                      int depth_bcast, const int* frame_idx, int count, long HW, void* out, int dtype,
                                       void* stream) {
   RDMI_REQUIRE(rgb && depth && frame_idx && out && count > 0, RDMI_E_ARG, "gather_unet_input: bad args");
   long n = (long)count * HW;
-  hipLaunchKernelGGL(gather_unet_input_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)rgb,
-                     rgb_frame_ld, (const f16*)depth, depth_frame_ld, depth_bcast, frame_idx, count, HW, (f16*)out);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(gather_unet_input_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)rgb, rgb_frame_ld, (const float*)depth, depth_frame_ld, depth_bcast, frame_idx,
+                       count, HW, (float*)out);
+  else
+    hipLaunchKernelGGL(gather_unet_input_k<f16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)rgb,
+                       rgb_frame_ld, (const f16*)depth, depth_frame_ld, depth_bcast, frame_idx, count, HW, (f16*)out);
   return rdmi::check_launch("gather_unet_input");
 }
 
 extern "C" int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* y, long ld_y, long P, int C,
-                                 int Cpad, float ca, float cb, float out_scale, long e_period, void* stream) {
+                                 int Cpad, float ca, float cb, float out_scale, long e_period, int dtype, void* stream) {
   RDMI_REQUIRE(x && e && y && Cpad >= C, RDMI_E_ARG, "ddim_combine: bad args");
   long n = P * Cpad;
-  hipLaunchKernelGGL(ddim_combine_k, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld_x,
-                     (const f16*)e, ld_e, (f16*)y, ld_y, P, C, Cpad, ca, cb, out_scale, e_period);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(ddim_combine_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       ld_x, (const float*)e, ld_e, (float*)y, ld_y, P, C, Cpad, ca, cb, out_scale, e_period);
+  else
+    hipLaunchKernelGGL(ddim_combine_k<f16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)x, ld_x,
+                       (const f16*)e, ld_e, (f16*)y, ld_y, P, C, Cpad, ca, cb, out_scale, e_period);
   return rdmi::check_launch("ddim_combine");
 }
 
@@ -334,13 +366,17 @@ extern "C" int rdmi_renormalize_f32(float* x, long n, const float* minmax, void*
 }
 
 extern "C" int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld, void* out,
-                                    void* stream) {
+                                    int dtype, void* stream) {
   RDMI_REQUIRE(src && out && n > 0 && w > 0 && N > 0 && ld >= C, RDMI_E_ARG, "snippet_average: bad args");
   long tot = P * ld;
   long gx = (tot + 255) / 256;
   if (gx > 4096) gx = 4096;
-  hipLaunchKernelGGL(snippet_average_k, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream, (const f16*)src, n, w,
-                     stride, P, C, ld, (f16*)out);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(snippet_average_k<float>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)src, n, w, stride, P, C, ld, (float*)out);
+  else
+    hipLaunchKernelGGL(snippet_average_k<f16>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream,
+                       (const f16*)src, n, w, stride, P, C, ld, (f16*)out);
   return rdmi::check_launch("snippet_average");
 }
 

@@ -317,30 +317,8 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
   }
 }
 
-// XCD-aware remap (T1): dispatch id d runs on XCD d % 8; give each XCD a contiguous range of
-// logical tiles so the n-tiles sharing one A row-panel share that XCD's L2.
-__device__ __forceinline__ int xcd_remap(int bid, int total) {
-  if (total < 8) return bid;
-  const int xcd = bid & 7, q = total >> 3, r = total & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
-// logical tile → (m-tile, n-tile): groups of G m-tiles sweep all n-tiles with m fastest, so the
-// tiles an XCD runs together share G A-panels and a few B-panels (L2 reuse in both operands)
-__device__ __forceinline__ void tile_mn(int logical, int nbx, int nby, int G, int& mt, int& nt) {
-  if (G <= 1) {
-    mt = logical / nbx;
-    nt = logical % nbx;
-    return;
-  }
-  const int per = G * nbx;
-  const int g = logical / per;
-  const int first = g * G;
-  const int gs = min(G, nby - first);
-  const int r = logical - g * per;
-  mt = first + r % gs;
-  nt = r / gs;
-}
+using rdmi::tile_mn;
+using rdmi::xcd_remap;
 
 // MODE 0: dense A [M, K] (Linear, 1×1 conv); MODE 1: implicit im2col of NHWC x for a 3×3 conv
 // (any stride/padding); MODE 2: 3×3 conv reading x through a nearest ×2 upsample.
@@ -1503,12 +1481,14 @@ bool in_gn_ok(const rdmi_conv_args* a) {
 }  // namespace
 
 extern "C" int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* a) {
-  return a && halo_eligible(a, halo_mode()) && in_gn_ok(a) ? 1 : 0;
+  return a && a->dtype == RDMI_F16 && halo_eligible(a, halo_mode()) && in_gn_ok(a) ? 1 : 0;
 }
 
 extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   RDMI_REQUIRE(a && a->A && a->W && a->C, RDMI_E_ARG, "gemm: null pointer");
   RDMI_REQUIRE(a->M > 0 && a->N > 0 && a->K > 0 && a->batch > 0, RDMI_E_ARG, "gemm: bad sizes M=%d N=%d K=%d", a->M, a->N, a->K);
+  RDMI_REQUIRE(a->dtype == RDMI_F16 || a->dtype == RDMI_F32, RDMI_E_UNSUPPORTED, "gemm: dtype %d", a->dtype);
+  if (a->dtype == RDMI_F32) return rdmi::gemm_f32(a, stream);
   RDMI_REQUIRE(a->K % 8 == 0 && a->lda % 8 == 0 && a->ldw % 8 == 0 && a->ldw >= a->K,
                RDMI_E_ALIGN, "gemm: K (%d), lda (%ld) must be multiples of 8 and ldw (%ld) >= K", a->K, a->lda, a->ldw);
   RDMI_REQUIRE(al16(a->A) && al16(a->W) && a->strideA % 8 == 0 && a->strideW % 8 == 0, RDMI_E_ALIGN, "gemm: A/W not 16-byte aligned");
@@ -1543,8 +1523,10 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
 
 extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   RDMI_REQUIRE(a && a->x && a->w && a->y, RDMI_E_ARG, "conv2d: null pointer");
-  RDMI_REQUIRE(a->Cin % 8 == 0, RDMI_E_ALIGN, "conv2d: Cin (%d) must be a multiple of 8", a->Cin);
   RDMI_REQUIRE(a->B > 0 && a->H > 0 && a->W > 0 && a->Cout > 0 && a->Ho > 0 && a->Wo > 0, RDMI_E_ARG, "conv2d: bad sizes");
+  RDMI_REQUIRE(a->dtype == RDMI_F16 || a->dtype == RDMI_F32, RDMI_E_UNSUPPORTED, "conv2d: dtype %d", a->dtype);
+  if (a->dtype == RDMI_F32) return rdmi::conv2d_f32(a, stream);
+  RDMI_REQUIRE(a->Cin % 8 == 0, RDMI_E_ALIGN, "conv2d: Cin (%d) must be a multiple of 8", a->Cin);
   const int K = a->kh * a->kw * a->Cin;
   RDMI_REQUIRE(a->Kp >= K && a->Kp % 8 == 0, RDMI_E_ARG, "conv2d: Kp (%d) must be >= %d and a multiple of 8", a->Kp, K);
   RDMI_REQUIRE(al16(a->x) && al16(a->w), RDMI_E_ALIGN, "conv2d: x/w not 16-byte aligned");

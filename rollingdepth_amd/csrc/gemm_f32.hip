@@ -1,0 +1,353 @@
+// f32 implicit-GEMM engine: the paper preset's fp32 arithmetic (run_video.py:444-449, dtype fp32)
+// for the same Linear / conv call sites as gemm.hip (rdmi_gemm / rdmi_conv2d with dtype RDMI_F32).
+//
+// gfx950 has no xf32: f32 inputs run on v_mfma_f32_16x16x4_f32 (exact f32 products, an f32 fmaf
+// chain per output; 64 FLOP/clk/SIMD = 157 TF, 1/16 of the f16 rate — MI355X_MICROARCH.md).  Each
+// 128×128 output tile is one 256-thread workgroup of 2×2 waves (64×64 per wave, 4×4 fragments of
+// 16×16).  K advances in 32-float K-tiles — one full 128-B line per operand row, the same byte
+// geometry as the f16 engine's 64-half K-tiles — through a 3-slot LDS ring filled by
+// buffer-load-to-LDS DMA (no VGPR staging, two K-tiles in flight, one barrier per K-tile); ragged
+// M / N / K and the conv's implicit zero padding are out-of-range buffer offsets (zeros).  16-B
+// chunk c of LDS row r sits at c ^ (r & 7) (swizzled on the DMA source side).
+// Fragment reads: lane quarter q (lane >> 4) supplies k = 8q + s at MFMA step s (s = 0..7 per
+// K-tile) for BOTH operands, so a lane reads its 8 k values as two 16-B chunks (2q, 2q+1) per
+// fragment instead of eight 4-B reads; the sum over k is the same set of products.
+// The MFMA runs as Dᵀ = W·Aᵀ, so a lane holds 4 consecutive output channels of one output row
+// (the f16 engine's epilogue geometry): bias / residual / output move as 16-B vectors.
+#include "common.h"
+
+namespace {
+
+constexpr int BKF = 32;  // K per stage (floats)
+
+struct GemmF32P {
+  const float* A; long lda, sA;
+  const float* Wt; long ldw, sW;
+  float* C; long ldc, sC;
+  const float* bias;
+  const float* R; long ldr, sR;
+  const float* rowbias; int rpg; long rb_ld;
+  float alpha;
+  int M, N, K, Kvalid;
+  int geglu, silu, vec;
+  unsigned a_bytes, w_bytes;
+  int IH, IW, Cin, Ho, Wo, stride, pt, pl, cin_vecs;
+  int group_m;
+};
+
+constexpr unsigned OOB = 0x80000000u;
+
+__device__ __forceinline__ void dma16f(__amdgpu_buffer_rsrc_t r, unsigned voff, float* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, 0, 0, 0);
+}
+
+// Epilogue: fragment (i, j) of a lane = output row mw + 16i + fr, channels nw + 16j + 4fq .. +3.
+template <int RM, int RN>
+__device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[RM][RN], int mw, int nw, int bz,
+                                               int fr, int fq) {
+  const long cb = (long)bz * p.sC;
+  const long rbz = (long)bz * p.sR;
+  if (!p.geglu) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int m = mw + i * 16 + fr;
+      if (m >= p.M) continue;
+      const float* rbrow = p.rowbias ? p.rowbias + (long)(m / p.rpg) * p.rb_ld : nullptr;
+      const long crow = cb + (long)m * p.ldc;
+      const long rrow = rbz + (long)m * p.ldr;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int n = nw + j * 16 + fq * 4;
+        if (n >= p.N) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * p.alpha;
+        if (p.vec && n + 3 < p.N) {
+          if (p.bias) {
+            const f32x4 bb = *(const f32x4*)(p.bias + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bb[r];
+          }
+          if (rbrow) {
+            const f32x4 bb = *(const f32x4*)(rbrow + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += bb[r];
+          }
+          if (p.R) {
+            const f32x4 rr = *(const f32x4*)(p.R + rrow + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += rr[r];
+          }
+          if (p.silu) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = v[r] / (1.0f + expf(-v[r]));
+          }
+          *(f32x4*)(p.C + crow + n) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nn = n + r;
+            if (nn >= p.N) break;
+            float x = v[r];
+            if (p.bias) x += p.bias[nn];
+            if (rbrow) x += rbrow[nn];
+            if (p.R) x += p.R[rrow + nn];
+            if (p.silu) x = x / (1.0f + expf(-x));
+            p.C[crow + nn] = x;
+          }
+        }
+      }
+    }
+  } else {
+    // GEGLU: within each wave's 64-column slab, columns [0,32) are the value half and [32,64) the
+    // gate half of output columns slab·32 + [0,32) (N % 128 == 0, weights row-interleaved).
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int m = mw + i * 16 + fr;
+      if (m >= p.M) continue;
+      const long crow = cb + (long)m * p.ldc;
+#pragma unroll
+      for (int j = 0; j < RN / 2; ++j) {
+        const int nh = nw + j * 16 + fq * 4;
+        const int no = nw / 2 + j * 16 + fq * 4;
+        const f32x4 bh = p.bias ? *(const f32x4*)(p.bias + nh) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 bg = p.bias ? *(const f32x4*)(p.bias + nh + 32) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float h = acc[i][j][r] * p.alpha + bh[r];
+          const float g = acc[i][j + RN / 2][r] * p.alpha + bg[r];
+          o[r] = h * gelu_erf(g);
+          if (p.R) o[r] += p.R[rbz + (long)m * p.ldr + no + r];
+        }
+        *(f32x4*)(p.C + crow + no) = o;
+      }
+    }
+  }
+}
+
+// MODE 0: dense A [M, K]; MODE 1: implicit im2col of an NHWC f32 tensor for a 3×3 conv (any stride /
+// padding, K order [tap][Cin]); MODE 2: the 3×3 conv reading x through a nearest ×2 upsample.
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
+  constexpr int BM = 128, BN = 128, NW = 4, WTM = 64, WTN = 64;
+  constexpr int RM = WTM / 16, RN = WTN / 16;
+  constexpr int AV = BM / 8 / NW, BV = BN / 8 / NW;  // 1-KiB DMA instructions per wave per K-tile
+  constexpr int LPS = AV + BV;
+  constexpr int SLOT = (BM + BN) * BKF;  // floats
+  __shared__ __attribute__((aligned(16))) float lds[3 * SLOT];  // 96 KiB
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nbx = gridDim.x;
+  const int logical = rdmi::xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+  int mt_, nt_;
+  rdmi::tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN, m0 = mt_ * BM;
+  const int bz = blockIdx.z;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.A + (long)bz * p.sA), (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.Wt + (long)bz * p.sW), (short)0, (int)p.w_bytes, 0x00020000);
+
+  const int lrow = lane >> 3;
+  const int chunk = (lane & 7) ^ lrow;  // logical 4-float chunk this lane fetches
+  int arow[AV], ahb[AV], awb[AV];
+#pragma unroll
+  for (int i = 0; i < AV; ++i) {
+    const int m = m0 + (i * NW + wid) * 8 + lrow;
+    const bool ok = m < p.M;
+    const int mm = ok ? m : 0;
+    if (MODE != 0) {
+      const int hw = p.Ho * p.Wo;
+      const int b = mm / hw;
+      const int r = mm - b * hw;
+      const int ho = r / p.Wo;
+      const int wo = r - ho * p.Wo;
+      const int hb = ho * p.stride - p.pt;
+      ahb[i] = ok ? hb : -(1 << 28);
+      awb[i] = wo * p.stride - p.pl;
+      arow[i] = MODE == 1 ? (b * p.IH + hb) * p.IW * p.Cin + awb[i] * p.Cin : b * p.IH * p.IW * p.Cin;
+    } else {
+      ahb[i] = ok ? 0 : -1;
+      awb[i] = 0;
+      arow[i] = mm * (int)p.lda;
+    }
+  }
+  int brow[BV];
+#pragma unroll
+  for (int i = 0; i < BV; ++i) {
+    const int n = n0 + (i * NW + wid) * 8 + lrow;
+    brow[i] = n < p.N ? n * (int)p.ldw : -1;
+  }
+  int tap = 0, cv = chunk;
+  if (MODE != 0) {
+    tap = chunk / p.cin_vecs;
+    cv = chunk - tap * p.cin_vecs;
+  }
+  const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
+
+  auto issue = [&](int ks, int slot) {
+    const int kk = ks * BKF + chunk * 4;
+    const bool kok = kk < p.Kvalid;
+    float* la = lds + slot * SLOT;
+    float* lb = la + BM * BKF;
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        const bool ok = ahb[i] == 0 && kok;
+        dma16f(ra_, ok ? (unsigned)(arow[i] + kk) * 4u : OOB, la + (i * NW + wid) * 8 * BKF);
+      }
+    } else {
+      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9
+      const int dx = tap - 3 * dy;
+      const int tapoff = (dy * p.IW + dx) * p.Cin + cv * 4;
+#pragma unroll
+      for (int i = 0; i < AV; ++i) {
+        const int hi = ahb[i] + dy, wi = awb[i] + dx;
+        const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
+        const int off = MODE == 1 ? arow[i] + tapoff : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cv * 4;
+        dma16f(ra_, ok ? (unsigned)off * 4u : OOB, la + (i * NW + wid) * 8 * BKF);
+      }
+      cv += 8;
+      while (cv >= p.cin_vecs) {
+        cv -= p.cin_vecs;
+        ++tap;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const bool ok = brow[i] >= 0 && kok;
+      dma16f(rw_, ok ? (unsigned)(brow[i] + kk) * 4u : OOB, lb + (i * NW + wid) * 8 * BKF);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BKF - 1) / BKF;
+  issue(0, 0);
+  issue(1, 1);
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    rdmi::wait_vmcnt_only<LPS>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(kt + 2, (kt + 2) % 3);
+    const float* la = lds + (kt % 3) * SLOT + (wm * WTM) * BKF;
+    const float* lb = lds + (kt % 3) * SLOT + BM * BKF + (wn * WTN) * BKF;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int lc = 2 * fq + h;  // logical chunk: k = 8·fq + 4h + (0..3)
+      f32x4 af[RM], bf[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int row = i * 16 + fr;
+        af[i] = *(const f32x4*)(la + row * BKF + ((lc ^ (row & 7)) << 2));
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int row = j * 16 + fr;
+        bf[j] = *(const f32x4*)(lb + row * BKF + ((lc ^ (row & 7)) << 2));
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(bf[j][s], af[i][s], acc[i][j], 0, 0, 0);
+    }
+  }
+  rdmi::wait_vmcnt_only<0>();
+  store_tile_f32<RM, RN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, bz, fr, fq);
+}
+
+bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+
+bool vec_ok(const GemmF32P& p) {
+  bool ok = p.ldc % 4 == 0 && p.sC % 4 == 0 && al16(p.C);
+  if (p.R) ok = ok && p.ldr % 4 == 0 && p.sR % 4 == 0 && al16(p.R);
+  if (p.bias) ok = ok && al16(p.bias);
+  if (p.rowbias) ok = ok && al16(p.rowbias) && p.rb_ld % 4 == 0;
+  return ok;
+}
+
+int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode) {
+  const char* gm = getenv("RDMI_GEMM_GROUP");
+  p.group_m = gm ? atoi(gm) : 8;
+  dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
+  if (mode == 2)
+    hipLaunchKernelGGL(gemm_f32_kernel<2>, g, dim3(256), 0, s, p);
+  else if (mode == 1)
+    hipLaunchKernelGGL(gemm_f32_kernel<1>, g, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(gemm_f32_kernel<0>, g, dim3(256), 0, s, p);
+  return rdmi::check_launch("gemm_f32");
+}
+
+}  // namespace
+
+namespace rdmi {
+
+int gemm_f32(const rdmi_gemm_args* a, void* stream) {
+  RDMI_REQUIRE(a->K % 4 == 0 && a->lda % 4 == 0 && a->ldw % 4 == 0 && a->ldw >= a->K, RDMI_E_ALIGN,
+               "gemm f32: K (%d), lda (%ld), ldw (%ld) must be multiples of 4 (ldw >= K)", a->K, a->lda, a->ldw);
+  RDMI_REQUIRE(al16(a->A) && al16(a->W) && a->strideA % 4 == 0 && a->strideW % 4 == 0, RDMI_E_ALIGN,
+               "gemm f32: A/W not 16-byte aligned");
+  RDMI_REQUIRE(a->epilogue != RDMI_EPI_GEGLU || a->N % 128 == 0, RDMI_E_ARG, "gemm f32: GEGLU needs N %% 128 == 0");
+  RDMI_REQUIRE(!a->rowbias || a->rows_per_group > 0, RDMI_E_ARG, "gemm f32: rowbias needs rows_per_group");
+  RDMI_REQUIRE(!a->gn_part, RDMI_E_UNSUPPORTED, "gemm f32: no GroupNorm moments (the groupnorm pass computes them)");
+  RDMI_REQUIRE((long)a->M * a->lda < (1L << 29) && (long)a->N * a->ldw < (1L << 29), RDMI_E_ARG,
+               "gemm f32: operand exceeds 2^29 elements (2 GiB) per batch");
+  GemmF32P p{};
+  p.A = (const float*)a->A; p.lda = a->lda; p.sA = a->strideA;
+  p.Wt = (const float*)a->W; p.ldw = a->ldw; p.sW = a->strideW;
+  p.C = (float*)a->C; p.ldc = a->ldc; p.sC = a->strideC;
+  p.bias = a->bias; p.R = (const float*)a->residual; p.ldr = a->ldr; p.sR = a->strideR;
+  p.rowbias = a->rowbias; p.rpg = a->rows_per_group > 0 ? a->rows_per_group : 1; p.rb_ld = a->rowbias_ld;
+  p.alpha = a->alpha;
+  p.M = a->M; p.N = a->N; p.K = (a->K + BKF - 1) / BKF * BKF; p.Kvalid = a->K;
+  p.geglu = a->epilogue == RDMI_EPI_GEGLU;
+  p.silu = a->epilogue == RDMI_EPI_SILU;
+  p.vec = vec_ok(p);
+  RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm f32: GEGLU output needs 4-element aligned rows");
+  p.a_bytes = (unsigned)(((long)(a->M - 1) * a->lda + a->K) * 4);
+  p.w_bytes = (unsigned)(((long)(a->N - 1) * a->ldw + a->K) * 4);
+  return launch_f32(p, a->batch, (hipStream_t)stream, 0);
+}
+
+int conv2d_f32(const rdmi_conv_args* a, void* stream) {
+  RDMI_REQUIRE(a->Cin % 4 == 0, RDMI_E_ALIGN, "conv2d f32: Cin (%d) must be a multiple of 4", a->Cin);
+  const int K = a->kh * a->kw * a->Cin;
+  RDMI_REQUIRE(a->Kp >= K && a->Kp % 4 == 0, RDMI_E_ARG, "conv2d f32: Kp (%d) must be >= %d, a multiple of 4", a->Kp, K);
+  RDMI_REQUIRE(al16(a->x) && al16(a->w), RDMI_E_ALIGN, "conv2d f32: x/w not 16-byte aligned");
+  RDMI_REQUIRE((long)a->B * a->H * a->W * a->Cin < (1L << 29) && (long)a->Cout * a->Kp < (1L << 29), RDMI_E_ARG,
+               "conv2d f32: input exceeds 2^29 elements (2 GiB; split the batch)");
+  RDMI_REQUIRE(!a->in_mean_rstd, RDMI_E_UNSUPPORTED, "conv2d f32: no fused input GroupNorm");
+  RDMI_REQUIRE(!a->gn_part, RDMI_E_UNSUPPORTED, "conv2d f32: no GroupNorm moments");
+  GemmF32P p{};
+  p.A = (const float*)a->x; p.Wt = (const float*)a->w; p.ldw = a->Kp;
+  p.C = (float*)a->y; p.ldc = a->y_ld > 0 ? a->y_ld : a->Cout;
+  p.bias = a->bias; p.R = (const float*)a->residual; p.ldr = a->res_ld > 0 ? a->res_ld : a->Cout;
+  p.rowbias = a->rowbias; p.rpg = a->Ho * a->Wo; p.rb_ld = a->rowbias_ld;
+  p.alpha = a->alpha;
+  p.M = a->B * a->Ho * a->Wo; p.N = a->Cout; p.K = (a->Kp + BKF - 1) / BKF * BKF; p.Kvalid = K;
+  p.IH = a->H; p.IW = a->W; p.Cin = a->Cin; p.Ho = a->Ho; p.Wo = a->Wo;
+  p.stride = a->stride; p.pt = a->pad_top; p.pl = a->pad_left; p.cin_vecs = a->Cin / 4;
+  const bool dense = a->kh == 1 && a->kw == 1 && a->stride == 1 && a->pad_top == 0 && a->pad_left == 0 && !a->upsample &&
+                     a->Ho == a->H && a->Wo == a->W;
+  if (dense) p.lda = a->Cin;
+  RDMI_REQUIRE(dense || (a->kh == 3 && a->kw == 3), RDMI_E_UNSUPPORTED, "conv2d f32: only 3x3 and dense 1x1 kernels");
+  RDMI_REQUIRE(!a->upsample || a->stride == 1, RDMI_E_UNSUPPORTED, "conv2d f32: upsample needs stride 1");
+  p.vec = vec_ok(p);
+  p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 4);
+  p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 4);
+  return launch_f32(p, 1, (hipStream_t)stream, dense ? 0 : (a->upsample ? 2 : 1));
+}
+
+}  // namespace rdmi

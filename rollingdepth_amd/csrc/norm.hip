@@ -13,7 +13,8 @@ constexpr int GN_MAX_SPLIT = 256;
 // streams its rows with four independent 16-B loads in flight and accumulates in f32 (at most a
 // few hundred rows per thread); the per-group combination of the threads' sums is f64 in a fixed
 // order.
-__global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__ x, long HW, int C, int G,
+template <typename T>
+__global__ __launch_bounds__(GN_THREADS) void gn_partial(const T* __restrict__ x, long HW, int C, int G,
                                                          int split, double* __restrict__ part) {
   const int CV = C >> 3;
   const int b = blockIdx.y;
@@ -24,7 +25,7 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__
   const int t = threadIdx.x;
   __shared__ float red[2][8][2][GN_THREADS];  // [colset][elem][sum,sumsq][thread] = 32 KB
   const int cpg = C / G;
-  const f16* xb = x + (long)b * HW * C;
+  const T* xb = x + (long)b * HW * C;
   for (int cs = 0; cs < 2; ++cs) {
     float s[8], ss[8];
 #pragma unroll
@@ -41,26 +42,27 @@ __global__ __launch_bounds__(GN_THREADS) void gn_partial(const f16* __restrict__
       active = cs == 0 && rl < RL;
     }
     if (active) {
-      const f16* xp = xb + cv * 8;
+      const T* xp = xb + cv * 8;
       long r = r0 + rl;
       for (; r + 3 * RL < r1; r += 4 * RL) {
-        f16x8 v[4];
+        float v[4][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *(const f16x8*)(xp + (r + u * RL) * C);
+        for (int u = 0; u < 4; ++u) ld8(xp + (r + u * RL) * C, v[u]);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float f = (float)v[u][e];
+            const float f = v[u][e];
             s[e] += f;
             ss[e] = fmaf(f, f, ss[e]);
           }
       }
       for (; r < r1; r += RL) {
-        const f16x8 v = *(const f16x8*)(xp + r * C);
+        float v[8];
+        ld8(xp + r * C, v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float f = (float)v[e];
+          const float f = v[e];
           s[e] += f;
           ss[e] = fmaf(f, f, ss[e]);
         }
@@ -167,7 +169,8 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
 
 // Streaming apply: each thread owns one 8-channel column (its 16 scale/shift values stay in
 // registers) and walks rows; no per-element division, 16-B loads/stores.
-__global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* __restrict__ y, long HW, int C,
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x, T* __restrict__ y, long HW, int C,
                                                 int G, int rows_per_block, const float* __restrict__ mr,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 int silu) {
@@ -176,14 +179,14 @@ __global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* 
   const int b = blockIdx.y;
   const long r0 = (long)blockIdx.x * rows_per_block;
   const long r1 = r0 + rows_per_block < HW ? r0 + rows_per_block : HW;
-  const int T = blockDim.x;
-  const int RL = CV >= T ? 1 : T / CV;
+  const int NT = blockDim.x;
+  const int RL = CV >= NT ? 1 : NT / CV;
   const int t = threadIdx.x;
-  const f16* xb = x + (long)b * HW * C;
-  f16* yb = y + (long)b * HW * C;
-  for (int cv0 = 0; cv0 < CV; cv0 += (CV >= T ? T : CV)) {
+  const T* xb = x + (long)b * HW * C;
+  T* yb = y + (long)b * HW * C;
+  for (int cv0 = 0; cv0 < CV; cv0 += (CV >= NT ? NT : CV)) {
     int cv, rl;
-    if (CV >= T) {
+    if (CV >= NT) {
       cv = cv0 + t;
       rl = 0;
       if (cv >= CV) break;
@@ -202,15 +205,15 @@ __global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* 
       sh[e] = beta[c] - mean * sc[e];
     }
     for (long r = r0 + rl; r < r1; r += RL) {
-      f16x8 in = *(const f16x8*)(xb + r * C + cv * 8);
-      f16x8 out;
+      float in[8], out[8];
+      ld8(xb + r * C + cv * 8, in);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float f = fmaf((float)in[e], sc[e], sh[e]);
-        if (silu) f = silu_f(f);
-        out[e] = (f16)f;
+        float f = fmaf(in[e], sc[e], sh[e]);
+        if (silu) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
+        out[e] = f;
       }
-      *(f16x8*)(yb + r * C + cv * 8) = out;
+      st8(yb + r * C + cv * 8, out);
     }
   }
 }
@@ -218,8 +221,8 @@ __global__ __launch_bounds__(256) void gn_apply(const f16* __restrict__ x, f16* 
 // one wave per row; C ≤ 64*8*4 = 2048
 // One wave per row, grid-stride over rows: the lane's columns are fixed, so gamma/beta live in
 // registers (loaded once per wave, not per row), and the next row is loaded one row ahead.
-template <int NV>  // f16x8 vectors per lane: C ≤ 512·NV
-__global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f16* __restrict__ y, long M, int C,
+template <typename T, int NV>  // 8-element vectors per lane: C ≤ 512·NV
+__global__ __launch_bounds__(256) void layernorm_k(const T* __restrict__ x, T* __restrict__ y, long M, int C,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                    float eps) {
   const int lane = threadIdx.x & 63;
@@ -237,26 +240,28 @@ __global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f1
   }
   const long stride = gridDim.x * 4L;
   long row = blockIdx.x * 4L + (threadIdx.x >> 6);
-  f16x8 vn[NV];
+  float vn[NV][8];
   auto load = [&](long r) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int cv = lane + 64 * i;
-      if (r < M && cv < CV) vn[i] = *(const f16x8*)(x + r * C + cv * 8);
+      if (r < M && cv < CV) ld8(x + r * C + cv * 8, vn[i]);
     }
   };
   load(row);
   for (; row < M; row += stride) {
-    f16x8 v[NV];
+    float v[NV][8];
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = vn[i];
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = vn[i][e];
     load(row + stride);
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
       if (lane + 64 * i < CV)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += (float)v[i][e];
+        for (int e = 0; e < 8; ++e) s += v[i][e];
     const float mean = wave_sum(s) / C;
     float q = 0.f;
 #pragma unroll
@@ -264,7 +269,7 @@ __global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f1
       if (lane + 64 * i < CV)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float d = (float)v[i][e] - mean;
+          const float d = v[i][e] - mean;
           q += d * d;
         }
     const float rstd = rsqrtf(wave_sum(q) / C + eps);
@@ -272,10 +277,10 @@ __global__ __launch_bounds__(256) void layernorm_k(const f16* __restrict__ x, f1
     for (int i = 0; i < NV; ++i) {
       const int cv = lane + 64 * i;
       if (cv < CV) {
-        f16x8 o;
+        float o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (f16)(((float)v[i][e] - mean) * rstd * gr[i][e] + br[i][e]);
-        *(f16x8*)(y + row * C + cv * 8) = o;
+        for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * gr[i][e] + br[i][e];
+        st8(y + row * C + cv * 8, o);
       }
     }
   }
@@ -295,7 +300,7 @@ int gn_split(int /*B*/, long HW, int C) {
 
 extern "C" long rdmi_groupnorm_workspace(int B, int G) { return (long)B * GN_MAX_SPLIT * G * 4; }
 
-extern "C" int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G, float eps, float* mean_rstd,
+extern "C" int rdmi_groupnorm_stats(const void* x, int dtype, int B, long HW, int C, int G, float eps, float* mean_rstd,
                                     float* workspace, void* stream) {
   RDMI_REQUIRE(x && mean_rstd && workspace, RDMI_E_ARG, "groupnorm_stats: null pointer");
   RDMI_REQUIRE(C % 8 == 0 && G > 0 && C % G == 0 && C <= 4096 && B > 0 && HW > 0, RDMI_E_ARG,
@@ -304,7 +309,10 @@ extern "C" int rdmi_groupnorm_stats(const void* x, int B, long HW, int C, int G,
   hipStream_t s = (hipStream_t)stream;
   int split = gn_split(B, HW, C);
   double* part = (double*)workspace;
-  hipLaunchKernelGGL(gn_partial, dim3(split, B), dim3(GN_THREADS), 0, s, (const f16*)x, HW, C, G, split, part);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(gn_partial<float>, dim3(split, B), dim3(GN_THREADS), 0, s, (const float*)x, HW, C, G, split, part);
+  else
+    hipLaunchKernelGGL(gn_partial<f16>, dim3(split, B), dim3(GN_THREADS), 0, s, (const f16*)x, HW, C, G, split, part);
   int rc = rdmi::check_launch("groupnorm_partial");
   if (rc) return rc;
   hipLaunchKernelGGL(gn_finalize, dim3(rdmi::div_up(B * G, 256)), dim3(256), 0, s, part, B, G, split,
@@ -323,7 +331,7 @@ extern "C" int rdmi_groupnorm_stats_partials(const float* part, long part_ld, in
   return rdmi::check_launch("groupnorm_stats_partials");
 }
 
-extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int C, int G, const float* mean_rstd,
+extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, long HW, int C, int G, const float* mean_rstd,
                                     const float* gamma, const float* beta, int silu, void* stream) {
   RDMI_REQUIRE(x && y && mean_rstd && gamma && beta, RDMI_E_ARG, "groupnorm_apply: null pointer");
   RDMI_REQUIRE(C % 8 == 0 && C % G == 0, RDMI_E_ARG, "groupnorm_apply: bad C=%d G=%d", C, G);
@@ -335,26 +343,38 @@ extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int B, long HW, int 
   if (rpb < RL) rpb = RL;
   rpb = (rpb + RL - 1) / RL * RL;
   dim3 g((unsigned)((HW + rpb - 1) / rpb), B);
-  hipLaunchKernelGGL(gn_apply, g, dim3(T), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
-                     mean_rstd, gamma, beta, silu);
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(gn_apply<float>, g, dim3(T), 0, (hipStream_t)stream, (const float*)x, (float*)y, HW, C, G,
+                       (int)rpb, mean_rstd, gamma, beta, silu);
+  else
+    hipLaunchKernelGGL(gn_apply<f16>, g, dim3(T), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
+                       mean_rstd, gamma, beta, silu);
   return rdmi::check_launch("groupnorm_apply");
 }
 
-extern "C" int rdmi_layernorm(const void* x, void* y, long M, int C, const float* gamma, const float* beta, float eps,
-                              void* stream) {
-  RDMI_REQUIRE(x && y && gamma && beta, RDMI_E_ARG, "layernorm: null pointer");
-  RDMI_REQUIRE(C % 8 == 0 && C <= 2048 && M > 0, RDMI_E_ARG, "layernorm: bad C=%d", C);
+template <typename T>
+int layernorm_launch(const void* x, void* y, long M, int C, const float* gamma, const float* beta, float eps,
+                     hipStream_t st) {
   long blocks = (M + 3) / 4;
   if (blocks > 4096) blocks = 4096;
   const int nv = (C / 8 + 63) / 64;
-  hipStream_t st = (hipStream_t)stream;
+  const T* xi = (const T*)x;
+  T* yo = (T*)y;
   if (nv == 1)
-    hipLaunchKernelGGL(layernorm_k<1>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+    hipLaunchKernelGGL((layernorm_k<T, 1>), dim3((unsigned)blocks), dim3(256), 0, st, xi, yo, M, C, gamma, beta, eps);
   else if (nv == 2)
-    hipLaunchKernelGGL(layernorm_k<2>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+    hipLaunchKernelGGL((layernorm_k<T, 2>), dim3((unsigned)blocks), dim3(256), 0, st, xi, yo, M, C, gamma, beta, eps);
   else if (nv == 3)
-    hipLaunchKernelGGL(layernorm_k<3>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+    hipLaunchKernelGGL((layernorm_k<T, 3>), dim3((unsigned)blocks), dim3(256), 0, st, xi, yo, M, C, gamma, beta, eps);
   else
-    hipLaunchKernelGGL(layernorm_k<4>, dim3((unsigned)blocks), dim3(256), 0, st, (const f16*)x, (f16*)y, M, C, gamma, beta, eps);
+    hipLaunchKernelGGL((layernorm_k<T, 4>), dim3((unsigned)blocks), dim3(256), 0, st, xi, yo, M, C, gamma, beta, eps);
   return rdmi::check_launch("layernorm");
+}
+
+extern "C" int rdmi_layernorm(const void* x, void* y, int dtype, long M, int C, const float* gamma, const float* beta,
+                              float eps, void* stream) {
+  RDMI_REQUIRE(x && y && gamma && beta, RDMI_E_ARG, "layernorm: null pointer");
+  RDMI_REQUIRE(C % 8 == 0 && C <= 2048 && M > 0, RDMI_E_ARG, "layernorm: bad C=%d", C);
+  if (dtype == RDMI_F32) return layernorm_launch<float>(x, y, M, C, gamma, beta, eps, (hipStream_t)stream);
+  return layernorm_launch<f16>(x, y, M, C, gamma, beta, eps, (hipStream_t)stream);
 }

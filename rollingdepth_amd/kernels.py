@@ -79,13 +79,21 @@ def _need(t: torch.Tensor, dtype, name: str):
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
 
 
+def _need_act(t: torch.Tensor, name: str):
+    """An activation of either storage dtype (f16 path, or the paper preset's f32 path)."""
+    if not t.is_cuda:
+        raise ValueError(f"{name}: expected a device tensor, got {t.device}")
+    if t.dtype not in (F16, F32):
+        raise TypeError(f"{name}: expected f16 or f32, got {t.dtype}")
+
+
 # ----------------------------------------------------------------------------- weight packing
-def pack_linear(w: torch.Tensor, device) -> torch.Tensor:
-    """[N, K] → f16 [N, Kp] (K zero-padded to a multiple of 32)."""
+def pack_linear(w: torch.Tensor, device, dtype=F16) -> torch.Tensor:
+    """[N, K] → [N, Kp] in the storage dtype (K zero-padded to a multiple of 32)."""
     n, k = w.shape
     kp = (k + 31) // 32 * 32
-    out = torch.zeros((n, kp), dtype=F16, device=device)
-    out[:, :k] = w.to(device=device, dtype=F16)
+    out = torch.zeros((n, kp), dtype=dtype, device=device)
+    out[:, :k] = w.to(device=device, dtype=dtype)
     return out
 
 
@@ -107,20 +115,20 @@ def pad_channels(c: int) -> int:
     return (c + 7) // 8 * 8
 
 
-def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> torch.Tensor:
-    """[Cout, Cin, kh, kw] → f16 [Cout, Kp] in the implicit-GEMM K order of gemm.hip (rdmi.h):
+def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16) -> torch.Tensor:
+    """[Cout, Cin, kh, kw] → [Cout, Kp] in the implicit-GEMM K order of gemm.hip (rdmi.h): f16:
     [Cout][Cin_pad/64][kh][kw][64] when kh·kw > 1 and Cin_pad % 64 == 0, else [Cout][kh][kw][Cin_pad];
-    zero padded to Kp % 32 == 0."""
+    f32 (gemm_f32.hip): always [Cout][kh][kw][Cin_pad]; zero padded to Kp % 32 == 0."""
     co, ci, kh, kw = w.shape
     cp = cin_pad or pad_channels(ci)
     t = torch.zeros((co, kh, kw, cp), dtype=F32)
     t[..., :ci] = w.permute(0, 2, 3, 1).float()
-    if kh * kw > 1 and cp % 64 == 0:
+    if dtype == F16 and kh * kw > 1 and cp % 64 == 0:
         t = t.reshape(co, kh, kw, cp // 64, 64).permute(0, 3, 1, 2, 4).contiguous()
     k = kh * kw * cp
     kp = (k + 31) // 32 * 32
-    out = torch.zeros((co, kp), dtype=F16)
-    out[:, :k] = t.reshape(co, k).half()
+    out = torch.zeros((co, kp), dtype=dtype)
+    out[:, :k] = t.reshape(co, k).to(dtype)
     return out.to(device)
 
 
@@ -134,8 +142,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     a: f16 [..., M, lda]; w: f16 [N, Kp]; batched over a leading dim when a is 3-D.
     gn=True: the epilogue also emits the GroupNorm moments of the output (see _gn_part), which a
     following `groupnorm(out, ...)` consumes instead of re-reading the tensor."""
-    _need(a, F16, "gemm.a")
-    _need(w, F16, "gemm.w")
+    _need_act(a, "gemm.a")
+    _need(w, a.dtype, "gemm.w")
+    f32 = a.dtype == F32
+    out_f32 = out_f32 or f32
     batch = a.shape[0] if a.dim() == 3 else 1
     M = a.shape[-2]
     N = w.shape[-2] if n is None else n
@@ -143,7 +153,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     if out is None:
         shape = (batch, M, NO) if a.dim() == 3 else (M, NO)
         out = torch.empty(shape, dtype=F32 if out_f32 else F16, device=a.device)
+    if residual is not None and residual.dtype != a.dtype:
+        raise TypeError("gemm: residual dtype must match the activations")
     g = _gemm_args(a, w, out, bias, residual, rowbias, rows_per_group, alpha, M, N, k, batch, geglu, out_f32)
+    g.dtype = _N.RDMI_F32 if f32 else _N.RDMI_F16
     if silu:
         g.epilogue = 2
     part = _gn_part(out, M, N) if (gn and batch == 1 and not geglu and not out_f32) else None
@@ -239,16 +252,19 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     gn=True: also emit the output's GroupNorm moments (as gemm).
     in_gn=(mean_rstd, gamma, beta, groups, silu): GroupNorm(+SiLU) of x applied as it is read
     (rdmi.h rdmi_conv_args.in_*; only where conv2d_in_gn_supported)."""
-    _need(x, F16, "conv2d.x")
-    _need(w, F16, "conv2d.w")
+    _need_act(x, "conv2d.x")
+    _need(w, x.dtype, "conv2d.w")
+    f32 = x.dtype == F32
     B, H, W, Cin = x.shape
     Ho, Wo = _out_hw(H, W, k, stride, pad, upsample, out_hw)
     if out is None:
-        out = torch.empty((B, Ho, Wo, cout), dtype=F16, device=x.device)
+        out = torch.empty((B, Ho, Wo, cout), dtype=x.dtype, device=x.device)
+    if f32:
+        gn, in_gn = False, None  # the f32 engine fuses neither (the groupnorm pass computes the moments)
     part = _gn_part(out, B * Ho * Wo, cout) if gn and _gn_slot is None else None
     if part is not None and not _split_slots_aligned(B, H * W * Cin, Ho * Wo):
         part = None  # some split level misaligns the moment slots: the next groupnorm computes them
-    if B > 1 and B * H * W * Cin >= (1 << 30):  # 32-bit buffer offsets: split the batch
+    if B > 1 and B * H * W * Cin >= _SPLIT_ELEMS[x.dtype]:  # 32-bit byte offsets: split the batch
         h = B // 2
         rb = rowbias if (rowbias is None or rowbias.dim() == 1) else None
         # GroupNorm-moment slots of the halves: carved from this call's buffer, or — when this call
@@ -272,6 +288,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
     a = _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn)
+    a.dtype = _N.RDMI_F32 if f32 else _N.RDMI_F16
     if part is not None:
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
@@ -284,8 +301,12 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     return out
 
 
+# conv2d splits its batch when the input reaches 2 GiB (the kernels' 32-bit buffer byte offsets)
+_SPLIT_ELEMS = {F16: 1 << 30, F32: 1 << 29}
+
+
 def _split_slots_aligned(B: int, elems_per_image: int, howo: int) -> bool:
-    """Whether every level of conv2d's recursive batch split (B > 1 and ≥ 2^30 input elements)
+    """Whether every level of conv2d's recursive batch split (B > 1 and ≥ 2^30 f16 input elements)
     starts its second half on a 32-row GroupNorm-moment slot boundary."""
     if B <= 1 or B * elems_per_image < (1 << 30):
         return True
@@ -301,6 +322,7 @@ def conv2d_in_gn_supported(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, 
     Ho, Wo = _out_hw(H, W, k, stride, pad, upsample, out_hw)
     a = _conv_args(x, w, cout, k, stride, pad, None, upsample, None, None, rowbias, None, 1.0, Ho, Wo,
                    (None, None, None, groups, 0))
+    a.dtype = _N.RDMI_F32 if x.dtype == F32 else _N.RDMI_F16
     return bool(lib.rdmi_conv2d_in_gn_supported(C.byref(a)))
 
 
@@ -336,7 +358,7 @@ def _workspace(n_floats: int, device) -> torch.Tensor:
 
 
 def groupnorm_stats(x: torch.Tensor, groups: int, eps: float) -> torch.Tensor:
-    _need(x, F16, "groupnorm.x")
+    _need_act(x, "groupnorm.x")
     B, C = x.shape[0], x.shape[-1]
     HW = x.numel() // (B * C)
     mr = torch.empty((B * groups * 2,), dtype=F32, device=x.device)
@@ -346,8 +368,8 @@ def groupnorm_stats(x: torch.Tensor, groups: int, eps: float) -> torch.Tensor:
                                                 _stream()), "rdmi_groupnorm_stats_partials")
         return mr
     ws = _workspace(lib.rdmi_groupnorm_workspace(B, groups), x.device)
-    check(lib.rdmi_groupnorm_stats(x.data_ptr(), B, HW, C, groups, eps, mr.data_ptr(), ws.data_ptr(), _stream()),
-          "rdmi_groupnorm_stats")
+    check(lib.rdmi_groupnorm_stats(x.data_ptr(), _dtype_code(x), B, HW, C, groups, eps, mr.data_ptr(), ws.data_ptr(),
+                                   _stream()), "rdmi_groupnorm_stats")
     return mr
 
 
@@ -358,8 +380,10 @@ def groupnorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
     HW = x.numel() // (B * C)
     out = torch.empty_like(x) if out is None else out
     _gn_attach(out, None)
-    check(lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), B, HW, C, groups, mr.data_ptr(), gamma.data_ptr(),
-                                   beta.data_ptr(), int(silu), _stream()), "rdmi_groupnorm_apply")
+    if out.dtype != x.dtype:
+        raise TypeError("groupnorm: out dtype must match x")
+    check(lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), _dtype_code(x), B, HW, C, groups, mr.data_ptr(),
+                                   gamma.data_ptr(), beta.data_ptr(), int(silu), _stream()), "rdmi_groupnorm_apply")
     return out
 
 
@@ -367,18 +391,18 @@ def conv3x3_to1_gn(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gro
                    w9: torch.Tensor, bias: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """GroupNorm(+SiLU) → 3×3 conv (pad 1) to one channel, fused (rdmi.h rdmi_conv3x3_to1_gn).
     x NHWC f16 [B, H, W, C]; w9 f32 [9, C] (tap = 3·dy + dx); returns [B, H, W, 1] f16."""
-    _need(x, F16, "conv3x3_to1_gn.x")
+    _need_act(x, "conv3x3_to1_gn.x")
     _need(w9, F32, "conv3x3_to1_gn.w9")
     B, H, W, C_ = x.shape
     if w9.shape != (9, C_):
         raise ValueError(f"conv3x3_to1_gn: w9 {tuple(w9.shape)} != (9, {C_})")
     mr = groupnorm_stats(x, groups, eps)
-    out = torch.empty((B, H, W, 1), dtype=F16, device=x.device) if out is None else out
-    if out.numel() != B * H * W or not out.is_contiguous():
+    out = torch.empty((B, H, W, 1), dtype=x.dtype, device=x.device) if out is None else out
+    if out.numel() != B * H * W or not out.is_contiguous() or out.dtype != x.dtype:
         raise ValueError("conv3x3_to1_gn: out must be a contiguous [B, H, W, 1] tensor")
     ws = _workspace(lib.rdmi_conv3x3_to1_gn_workspace(B, H, W), x.device)
     with _Timed("conv_head", 2.0 * 9 * C_ * B * H * W, f"head B={B} {H}x{W} {C_}->1"):
-        check(lib.rdmi_conv3x3_to1_gn(x.data_ptr(), B, H, W, C_, groups, mr.data_ptr(), gamma.data_ptr(),
+        check(lib.rdmi_conv3x3_to1_gn(x.data_ptr(), _dtype_code(x), B, H, W, C_, groups, mr.data_ptr(), gamma.data_ptr(),
                                       beta.data_ptr(), int(silu), w9.data_ptr(), float(bias), out.data_ptr(),
                                       ws.data_ptr(), _stream()), "rdmi_conv3x3_to1_gn")
     return out
@@ -386,12 +410,12 @@ def conv3x3_to1_gn(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gro
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-5,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    _need(x, F16, "layernorm.x")
+    _need_act(x, "layernorm.x")
     C_ = x.shape[-1]
     M = x.numel() // C_
     out = torch.empty_like(x) if out is None else out
-    check(lib.rdmi_layernorm(x.data_ptr(), out.data_ptr(), M, C_, gamma.data_ptr(), beta.data_ptr(), eps, _stream()),
-          "rdmi_layernorm")
+    check(lib.rdmi_layernorm(x.data_ptr(), out.data_ptr(), _dtype_code(x), M, C_, gamma.data_ptr(), beta.data_ptr(), eps,
+                             _stream()), "rdmi_layernorm")
     return out
 
 
@@ -399,20 +423,22 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
 def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out: Optional[torch.Tensor] = None,
               scale: Optional[float] = None) -> torch.Tensor:
     """q/k/v: f16 [B, S, H*64] views (any row stride, unit column stride) → out [B, Sq, H*64]."""
+    _need_act(q, "attention.q")
     for t, nm in ((q, "q"), (k, "k"), (v, "v")):
-        _need(t, F16, f"attention.{nm}")
+        _need(t, q.dtype, f"attention.{nm}")
         if t.stride(-1) != 1:
             raise ValueError("attention: inner dim must be contiguous")
     B, Sq, HD = q.shape
     D = HD // heads
     Sk = k.shape[1]
     if out is None:
-        out = torch.empty((B, Sq, HD), dtype=F16, device=q.device)
+        out = torch.empty((B, Sq, HD), dtype=q.dtype, device=q.device)
     sc = 1.0 / math.sqrt(D) if scale is None else scale
-    with _Timed("attention_fwd", 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}"):
+    name = "attention_fwd" if q.dtype == F16 else "attention_fwd_f32"
+    with _Timed(name, 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}"):
         check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
                                      q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
-                                     v.stride(0), out.stride(0), sc, _stream()), "rdmi_attention_fwd")
+                                     v.stride(0), out.stride(0), sc, _dtype_code(q), _stream()), "rdmi_attention_fwd")
     return out
 
 
@@ -448,100 +474,105 @@ def cross_attn_pair(x: torch.Tensor, ln_g: torch.Tensor, ln_b: torch.Tensor, eps
 def attention_smallkv(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """q [B, Sq, H*64] (row stride any), k/v [Bkv, L, H*64] contiguous with Bkv ∈ {1, B}."""
-    _need(q, F16, "attention_smallkv.q")
+    _need_act(q, "attention_smallkv.q")
+    _need(k, q.dtype, "attention_smallkv.k")
+    _need(v, q.dtype, "attention_smallkv.v")
     B, Sq, HD = q.shape
     D = HD // heads
     L = k.shape[1]
     k = k.contiguous()
     v = v.contiguous()
     if out is None:
-        out = torch.empty((B, Sq, HD), dtype=F16, device=q.device)
+        out = torch.empty((B, Sq, HD), dtype=q.dtype, device=q.device)
     kv_bs = 0 if k.shape[0] == 1 else k.stride(0)
     check(lib.rdmi_attention_smallkv(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, L, D,
                                      q.stride(1), out.stride(1), q.stride(0), out.stride(0), kv_bs,
-                                     1.0 / math.sqrt(D), _stream()), "rdmi_attention_smallkv")
+                                     1.0 / math.sqrt(D), _dtype_code(q), _stream()), "rdmi_attention_smallkv")
     return out
 
 
-def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """f32 scores [..., cols] → f16 probabilities; `out` may be wider (row stride p_ld ≥ cols: the
-    extra columns are written as zeros)."""
+def softmax_rows(s: torch.Tensor, scale: float, out: Optional[torch.Tensor] = None, dtype=F16) -> torch.Tensor:
+    """f32 scores [..., cols] → probabilities in `dtype` (or out's dtype); `out` may be wider (row
+    stride p_ld ≥ cols: the extra columns are written as zeros)."""
     _need(s, F32, "softmax_rows.s")
     cols = s.shape[-1]
     rows = s.numel() // cols
-    out = torch.empty(s.shape, dtype=F16, device=s.device) if out is None else out
+    out = torch.empty(s.shape, dtype=dtype, device=s.device) if out is None else out
     p_ld = out.shape[-1]
     if out.numel() != rows * p_ld or not out.is_contiguous() or p_ld < cols:
         raise ValueError("softmax_rows: out must be a contiguous [..., >= cols] tensor")
-    check(lib.rdmi_softmax_rows(s.data_ptr(), out.data_ptr(), rows, cols, p_ld, scale, _stream()), "rdmi_softmax_rows")
+    check(lib.rdmi_softmax_rows(s.data_ptr(), out.data_ptr(), rows, cols, p_ld, scale, _dtype_code(out), _stream()),
+          "rdmi_softmax_rows")
     return out
 
 
 def attention_1head(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:
     """Single-head attention for any head dim (the VAE mid-block, d = C): f32 scores GEMM → row
-    softmax → PV GEMM.  q [B, Sq, D], k/v [B, Sk, D] (row strides any, 16-B aligned) → [B, Sq, D].
-    A key count that is not a multiple of 8 runs the PV GEMM on K padded with zero probabilities."""
+    softmax → PV GEMM.  q [B, Sq, D], k/v [B, Sk, D] (row strides any, 16-B aligned) → [B, Sq, D],
+    in q's dtype.  A key count that is not a multiple of 8 runs the PV GEMM on K padded with zero
+    probabilities."""
     B, Sq, D = q.shape
     Sk = k.shape[1]
     s = gemm(q, k, D, out_f32=True)
     Sp = (Sk + 7) // 8 * 8
-    p = softmax_rows(s, scale, out=torch.empty((B, Sq, Sp), dtype=F16, device=q.device))
+    p = softmax_rows(s, scale, out=torch.empty((B, Sq, Sp), dtype=q.dtype, device=q.device))
     del s
-    vt = torch.zeros((B, D, Sp), dtype=F16, device=q.device) if Sp != Sk else None
+    vt = torch.zeros((B, D, Sp), dtype=q.dtype, device=q.device) if Sp != Sk else None
     vt = transpose(v, out=vt)
     return gemm(p, vt, Sp)
 
 
 def transpose(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[B, R, Cc] (row stride any) → [B, Cc, R] contiguous."""
-    _need(src, F16, "transpose.src")
+    _need_act(src, "transpose.src")
     B, R, Cc = src.shape
-    out = torch.empty((B, Cc, R), dtype=F16, device=src.device) if out is None else out
-    check(lib.rdmi_transpose(src.data_ptr(), out.data_ptr(), B, R, Cc, src.stride(1), out.stride(1), _stream()),
-          "rdmi_transpose")
+    out = torch.empty((B, Cc, R), dtype=src.dtype, device=src.device) if out is None else out
+    check(lib.rdmi_transpose(src.data_ptr(), out.data_ptr(), B, R, Cc, src.stride(1), out.stride(1), _dtype_code(src),
+                             _stream()), "rdmi_transpose")
     return out
 
 
 # ----------------------------------------------------------------------------- layout / misc
-def nchw_to_nhwc(x: torch.Tensor, cpad: int, scale: float = 1.0) -> torch.Tensor:
-    """[B, C, H, W] (any batch/channel strides, e.g. a stride-0 channel repeat) → NHWC f16."""
+def nchw_to_nhwc(x: torch.Tensor, cpad: int, scale: float = 1.0, dtype=F16) -> torch.Tensor:
+    """[B, C, H, W] (any batch/channel strides, e.g. a stride-0 channel repeat) → NHWC in `dtype`."""
     if not x.is_cuda or x.dtype not in (F16, F32):
         raise TypeError("nchw_to_nhwc: device f16/f32 tensor expected")
     B, Cc, H, W = x.shape
     if x.stride(3) != 1 or x.stride(2) != W:
         x = x.contiguous()
-    out = torch.empty((B, H, W, cpad), dtype=F16, device=x.device)
-    check(lib.rdmi_nchw_to_nhwc(x.data_ptr(), int(x.dtype == F32), out.data_ptr(), B, Cc, H, W, cpad, scale,
-                                x.stride(0), x.stride(1), _stream()), "rdmi_nchw_to_nhwc")
+    out = torch.empty((B, H, W, cpad), dtype=dtype, device=x.device)
+    check(lib.rdmi_nchw_to_nhwc(x.data_ptr(), int(x.dtype == F32), out.data_ptr(), _dtype_code(out), B, Cc, H, W, cpad,
+                                scale, x.stride(0), x.stride(1), _stream()), "rdmi_nchw_to_nhwc")
     return out
 
 
 def nhwc_to_nchw_f32(x: torch.Tensor, c: int, scale: float = 1.0, shift: float = 0.0) -> torch.Tensor:
-    _need(x, F16, "nhwc_to_nchw.x")
+    _need_act(x, "nhwc_to_nchw.x")
     B, H, W, Cl = x.shape
     out = torch.empty((B, c, H, W), dtype=F32, device=x.device)
-    check(lib.rdmi_nhwc_to_nchw_f32(x.data_ptr(), x.stride(2), out.data_ptr(), B, c, H, W, scale, shift, _stream()),
-          "rdmi_nhwc_to_nchw_f32")
+    check(lib.rdmi_nhwc_to_nchw_f32(x.data_ptr(), _dtype_code(x), x.stride(2), out.data_ptr(), B, c, H, W, scale, shift,
+                                    _stream()), "rdmi_nhwc_to_nchw_f32")
     return out
 
 
 def concat_channels(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    _need(a, F16, "concat.a")
-    _need(b, F16, "concat.b")
+    _need_act(a, "concat.a")
+    _need(b, a.dtype, "concat.b")
     Ca, Cb = a.shape[-1], b.shape[-1]
     P = a.numel() // Ca
-    out = torch.empty((*a.shape[:-1], Ca + Cb), dtype=F16, device=a.device) if out is None else out
-    check(lib.rdmi_concat_channels(a.data_ptr(), Ca, b.data_ptr(), Cb, out.data_ptr(), P, _stream()), "rdmi_concat")
+    out = torch.empty((*a.shape[:-1], Ca + Cb), dtype=a.dtype, device=a.device) if out is None else out
+    check(lib.rdmi_concat_channels(a.data_ptr(), Ca, b.data_ptr(), Cb, out.data_ptr(), P, _dtype_code(a), _stream()),
+          "rdmi_concat")
     return out
 
 
 def resize_nearest(x: torch.Tensor, size, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """NHWC f16 [B, H, W, C] → [B, Ho, Wo, C], F.interpolate(size=(Ho, Wo), mode="nearest")."""
-    _need(x, F16, "resize_nearest.x")
+    """NHWC [B, H, W, C] → [B, Ho, Wo, C], F.interpolate(size=(Ho, Wo), mode="nearest")."""
+    _need_act(x, "resize_nearest.x")
     B, H, W, C_ = x.shape
     Ho, Wo = size
-    out = torch.empty((B, Ho, Wo, C_), dtype=F16, device=x.device) if out is None else out
-    check(lib.rdmi_resize_nearest(x.data_ptr(), B, H, W, C_, out.data_ptr(), Ho, Wo, _stream()),
+    out = torch.empty((B, Ho, Wo, C_), dtype=x.dtype, device=x.device) if out is None else out
+    check(lib.rdmi_resize_nearest(x.data_ptr(), B, H, W, C_, out.data_ptr(), Ho, Wo, _dtype_code(x), _stream()),
           "rdmi_resize_nearest")
     return out
 
@@ -549,13 +580,14 @@ def resize_nearest(x: torch.Tensor, size, out: Optional[torch.Tensor] = None) ->
 def gather_unet_input(rgb: torch.Tensor, depth: torch.Tensor, frame_idx: torch.Tensor, depth_bcast: bool,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """rgb [N, h, w, 8] (channels 0..3 used), depth [N or 1, h, w, 8]; frame_idx int32 device."""
-    _need(rgb, F16, "gather.rgb")
+    _need_act(rgb, "gather.rgb")
+    _need(depth, rgb.dtype, "gather.depth")
     cnt = frame_idx.numel()
     _, h, w, _c = rgb.shape
-    out = torch.empty((cnt, h, w, 8), dtype=F16, device=rgb.device) if out is None else out
+    out = torch.empty((cnt, h, w, 8), dtype=rgb.dtype, device=rgb.device) if out is None else out
     check(lib.rdmi_gather_unet_input(rgb.data_ptr(), rgb.stride(0), depth.data_ptr(), depth.stride(0),
-                                     int(depth_bcast), frame_idx.data_ptr(), cnt, h * w, out.data_ptr(), _stream()),
-          "rdmi_gather_unet_input")
+                                     int(depth_bcast), frame_idx.data_ptr(), cnt, h * w, out.data_ptr(),
+                                     _dtype_code(rgb), _stream()), "rdmi_gather_unet_input")
     return out
 
 
@@ -563,26 +595,28 @@ def ddim_combine(x: torch.Tensor, e: torch.Tensor, ca: float, cb: float, out_sca
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y[..., :c] = (ca·x + cb·e)·out_scale, y[..., c:cpad] = 0; x/e channel-last views [.., P, ld].
     If e has fewer pixel rows than x (e.g. one noise frame), it is broadcast periodically."""
+    _need_act(x, "ddim_combine.x")
+    _need(e, x.dtype, "ddim_combine.e")
     P = x.numel() // x.shape[-1]
     Pe = e.numel() // e.shape[-1]
     period = 0 if Pe == P else Pe
     if period and P % Pe:
         raise ValueError("ddim_combine: broadcast operand must tile the sample")
-    out = torch.empty((*x.shape[:-1], cpad), dtype=F16, device=x.device) if out is None else out
+    out = torch.empty((*x.shape[:-1], cpad), dtype=x.dtype, device=x.device) if out is None else out
     check(lib.rdmi_ddim_combine(x.data_ptr(), x.stride(-2) if x.dim() >= 2 else x.shape[-1], e.data_ptr(),
                                 e.stride(-2) if e.dim() >= 2 else e.shape[-1], out.data_ptr(), out.stride(-2), P, c, cpad,
-                                ca, cb, out_scale, period, _stream()), "rdmi_ddim_combine")
+                                ca, cb, out_scale, period, _dtype_code(x), _stream()), "rdmi_ddim_combine")
     return out
 
 
 def snippet_average(src: torch.Tensor, stride: int, N: int, c: int = 4) -> torch.Tensor:
-    """src [n, w, h, wd, ld] f16 → [N, h, wd, ld] mean over covering snippets (refine)."""
-    _need(src, F16, "snippet_average.src")
+    """src [n, w, h, wd, ld] → [N, h, wd, ld] mean over covering snippets (refine)."""
+    _need_act(src, "snippet_average.src")
     n, w, h, wd, ld = src.shape
     src = src.contiguous()
-    out = torch.empty((N, h, wd, ld), dtype=F16, device=src.device)
-    check(lib.rdmi_snippet_average(src.data_ptr(), n, w, stride, N, h * wd, c, ld, out.data_ptr(), _stream()),
-          "rdmi_snippet_average")
+    out = torch.empty((N, h, wd, ld), dtype=src.dtype, device=src.device)
+    check(lib.rdmi_snippet_average(src.data_ptr(), n, w, stride, N, h * wd, c, ld, out.data_ptr(), _dtype_code(src),
+                                   _stream()), "rdmi_snippet_average")
     return out
 
 

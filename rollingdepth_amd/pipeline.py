@@ -111,12 +111,13 @@ class RollingDepthPipeline:
     def from_pretrained(cls, path: str, torch_dtype=torch.float16, device="cuda", **kw) -> "RollingDepthPipeline":
         """Diffusers-format checkpoint directory (model_index.json, unet/, vae/, scheduler/;
         pipeline_utils.py:480).  Weights via safetensors (or torch.load(weights_only=True))."""
-        if torch_dtype not in (torch.float16, None):
-            raise NotImplementedError("this build runs the f16 path (f32 kernels: next round)")
+        dtype = torch.float16 if torch_dtype is None else torch_dtype
+        if dtype not in (torch.float16, torch.float32):
+            raise NotImplementedError(f"torch_dtype {torch_dtype}: the HIP path runs float16 or float32")
         rd = lambda sub: json.load(open(os.path.join(path, sub, "config.json" if sub != "scheduler" else "scheduler_config.json")))
         ucfg, vcfg, scfg = rd("unet"), rd("vae"), rd("scheduler")
-        unet = UNet(ucfg, _load_state_dict(os.path.join(path, "unet")), device)
-        vae = VAE(vcfg, _load_state_dict(os.path.join(path, "vae")), device)
+        unet = UNet(ucfg, _load_state_dict(os.path.join(path, "unet")), device, dtype)
+        vae = VAE(vcfg, _load_state_dict(os.path.join(path, "vae")), device, dtype)
         pipe = cls(unet, vae, DDIMScheduler.from_config(scfg))
         emb = os.path.join(path, "empty_text_embed.safetensors")
         if os.path.exists(emb):
@@ -126,11 +127,11 @@ class RollingDepthPipeline:
 
     @classmethod
     def from_synthetic(cls, unet_cfg=SD2_UNET, vae_cfg=SD2_VAE, sched_cfg=RD_SCHEDULER, seed: int = 0,
-                       device="cuda") -> "RollingDepthPipeline":
+                       device="cuda", torch_dtype=torch.float16) -> "RollingDepthPipeline":
         """Random-init weights of the architecture (no checkpoint in the image), deterministic
         per state-dict key (weights.py) — identical to what the golden fixtures used."""
-        unet = UNet(unet_cfg, Wt.synth_state_dict(Wt.unet_param_shapes(unet_cfg), seed), device)
-        vae = VAE(vae_cfg, Wt.synth_state_dict(Wt.vae_param_shapes(vae_cfg), seed), device)
+        unet = UNet(unet_cfg, Wt.synth_state_dict(Wt.unet_param_shapes(unet_cfg), seed), device, torch_dtype)
+        vae = VAE(vae_cfg, Wt.synth_state_dict(Wt.vae_param_shapes(vae_cfg), seed), device, torch_dtype)
         pipe = cls(unet, vae, DDIMScheduler.from_config(sched_cfg))
         pipe.empty_text_embed = Wt.synth_context(unet_cfg["cross_attention_dim"], seed)
         return pipe
@@ -141,7 +142,7 @@ class RollingDepthPipeline:
 
     @property
     def dtype(self):
-        return F16
+        return self.unet.dtype
 
     def to(self, *args, **kwargs):
         """DiffusionPipeline.to (pipeline_utils.py:303): weights already live on the device the
@@ -238,16 +239,16 @@ class RollingDepthPipeline:
         n = init_noise if init_noise.dim() == 4 else init_noise[None]
         if tuple(n.shape) != (1, self.N_CHANNEL_PER_LATENT, h, w):
             raise ValueError(f"init_noise shape {tuple(init_noise.shape)} != (1, 4, {h}, {w}) (the latent size)")
-        return K.nchw_to_nhwc(n.to(self.device), 8)
+        return K.nchw_to_nhwc(n.to(self.device), 8, dtype=self.dtype)
 
     # ------------------------------------------------------------------ stages
     def encode_rgb(self, frames_nchw: torch.Tensor) -> torch.Tensor:
         """[N,3,H,W] in [-1,1] (any float dtype, on device) → NHWC f16 [N, h, w, 8] latents·0.18215."""
         N, _, H, W = frames_nchw.shape
         h, w = self.vae.latent_hw(H, W)
-        out = torch.zeros((N, h, w, self.vae.lat_pad), dtype=F16, device=self.device)
+        out = torch.zeros((N, h, w, self.vae.lat_pad), dtype=self.dtype, device=self.device)
         for i0, i1 in self._vae_chunks(N, h, w):
-            x = K.nchw_to_nhwc(frames_nchw[i0:i1], self.vae.in_pad)
+            x = K.nchw_to_nhwc(frames_nchw[i0:i1], self.vae.in_pad, dtype=self.dtype)
             self.vae.encode(x, out=out[i0:i1])
         return out
 
@@ -257,7 +258,9 @@ class RollingDepthPipeline:
         (768²: 75 frames; 1024²: 30).  Measured at 768² (75-frame snippet batches): 16 → 21.0,
         38 → 21.1, 75 → 21.2 depth frames/s (profiles/r01_vae_batch_ab.log)."""
         hw = h * w
-        cap = min(self.vae_batch, max(1, int(32e9 // (hw * hw * 4))), max(1, int(24e9 // (hw * 64 * 128 * 2))))
+        esz = self.dtype.itemsize  # (f32 path: the probabilities are f32 too, and every activation doubles)
+        cap = min(self.vae_batch, max(1, int(32e9 // (hw * hw * (4 + esz)))),
+                  max(1, int(24e9 // (hw * 64 * 128 * esz))))
         return _balanced(n, cap)
 
     def decode_depth(self, z_scaled: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
@@ -271,7 +274,7 @@ class RollingDepthPipeline:
             self.encode_empty_text()
         ctx = self.empty_text_embed
         if getattr(self, "_ctx16_src", None) is not ctx:
-            self._ctx16 = ctx.to(self.device, F16).contiguous()
+            self._ctx16 = ctx.to(self.device, self.dtype).contiguous()
             self._ctx16_src = ctx
             self.unet.set_context(self._ctx16)
         return self._ctx16
@@ -283,7 +286,8 @@ class RollingDepthPipeline:
         UNet activation — the [b·slen·h·w, 4·C0] GEGLU output feeding ff2 — below 2^31 bytes (the
         kernels' 32-bit buffer offsets): 30 snippets at 96², 17 at 128²."""
         c0 = int(self.unet.cfg["block_out_channels"][0])
-        return _balanced(n, max(1, min(self.snippet_batch, (2 ** 31 - 1) // (slen * h * w * 4 * c0 * 2))))
+        esz = self.dtype.itemsize
+        return _balanced(n, max(1, min(self.snippet_batch, (2 ** 31 - 1) // (slen * h * w * 4 * c0 * esz))))
 
     def init_snippet_infer(self, rgb_latent: torch.Tensor, init_noise: torch.Tensor, dilations: List[int],
                            snippet_lengths: List[int], init_infer_steps: List[int], strides: List[int],
@@ -302,7 +306,7 @@ class RollingDepthPipeline:
             idx = self.get_snippet_indice(0, timesteps, N, slen, dil, dil, stride)
             todo = list(range(len(idx))) if snippet_subset is None else list(snippet_subset[di])
             # row r of the output is snippet todo[r] (all snippets unless a subset is given)
-            buf = torch.empty((len(todo), slen, H, W), dtype=F16, device=self.device)
+            buf = torch.empty((len(todo), slen, H, W), dtype=self.dtype, device=self.device)
             fidx_all = self._device_index([f for s in todo for f in idx[s]]) if todo else None
             for b0, b1 in self._snippet_batches(len(todo), slen, h, w):
                 sel = todo[b0:b1]
@@ -315,13 +319,13 @@ class RollingDepthPipeline:
                     if last:
                         zin = self.scheduler.step_(pred, int(t), depth_view, 1.0 / self.depth_latent_scale_factor,
                                                    channels=self.N_CHANNEL_PER_LATENT,
-                                                   out=torch.empty((x.shape[0], h, w, 8), dtype=F16,
+                                                   out=torch.empty((x.shape[0], h, w, 8), dtype=self.dtype,
                                                                    device=self.device))
                         if record is not None:
                             record.setdefault("unet_out", []).append(pred)
                             record.setdefault("snippet_latent", []).append(
                                 self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4,
-                                                     out=torch.empty((x.shape[0], h, w, 8), dtype=F16,
+                                                     out=torch.empty((x.shape[0], h, w, 8), dtype=self.dtype,
                                                                      device=self.device)))
                     else:
                         x2 = x.clone()
@@ -365,7 +369,7 @@ class RollingDepthPipeline:
             assert len(covered) == N, "refine: every frame must be covered by a snippet"
             lo, hi = _contiguous_range(len(idx), world, rank)
             mine = idx[lo:hi]
-            preds = torch.empty((len(mine), snippet_len, h, w, 8), dtype=F16, device=self.device)
+            preds = torch.empty((len(mine), snippet_len, h, w, 8), dtype=self.dtype, device=self.device)
             fidx_all = self._device_index([f for s in mine for f in s]) if mine else None
             for b0, b1 in self._snippet_batches(len(mine), snippet_len, h, w):
                 sel = mine[b0:b1]
@@ -380,7 +384,7 @@ class RollingDepthPipeline:
                 import torch.distributed as dist
                 sums = K.snippet_accumulate(preds, lo, stride, N)
                 dist.all_reduce(sums, group=group)
-                new = K.snippet_finish(sums, len(idx), snippet_len, stride, (h, w), 8)
+                new = K.snippet_finish(sums, len(idx), snippet_len, stride, (h, w), 8, dtype=self.dtype)
         return new
 
     # ------------------------------------------------------------------ entry points
@@ -431,7 +435,7 @@ class RollingDepthPipeline:
         H, W = so.depth_pred_full.shape[-2:]
         d2h = torch.cuda.Stream(self.device)
         snip_host = [self._to_host_async(s.view(s.shape[0], s.shape[1], 1, H, W), d2h) for s in snips]
-        rgb = input_frames[0].to(self.device, F16) / 2.0 + 0.5
+        rgb = input_frames[0].to(self.device, self.dtype) / 2.0 + 0.5
         outs = [self._to_host_async(t, d2h) for t in (rgb, so.depth_pred_full, so.depth_coaligned_full)]
         d2h.synchronize()
         return RollingDepthOutput(input_rgb=outs[0], depth_pred=outs[1], snippet_ls=snip_host,
@@ -480,7 +484,7 @@ class RollingDepthPipeline:
         N, h, w, _ = rgb_latent.shape
         # ----------------- shared init noise (:282-288)
         if init_noise is None:
-            init_noise = torch.randn((1, 4, h, w), device=self.device, dtype=F16, generator=generator)
+            init_noise = torch.randn((1, 4, h, w), device=self.device, dtype=self.dtype, generator=generator)
         noise = self._noise_nhwc(init_noise, h, w)
         snippets = self.init_snippet_infer(rgb_latent, noise, dilations, snippet_lengths, init_infer_steps, strides,
                                            record=record)
@@ -494,7 +498,7 @@ class RollingDepthPipeline:
                                                   dilations)
         d = merged.float().contiguous()
         K.renormalize_(d, K.minmax(d))
-        coaligned = d.to(F16)
+        coaligned = d.to(self.dtype)
         if record is not None:
             record.update(rgb_latent=rgb_latent, scales=scales, translations=trans, loss_history=hist,
                           dilations=list(dilations))
@@ -505,7 +509,7 @@ class RollingDepthPipeline:
             if record is not None:
                 record["refined_latent"] = new
             z = K.ddim_combine(new[..., :4], new[..., :4], 1.0 / self.depth_latent_scale_factor, 0.0, 1.0, 4, 8)
-            dec = torch.empty((N, H, W, 1), dtype=F16, device=self.device)
+            dec = torch.empty((N, H, W, 1), dtype=self.dtype, device=self.device)
             self.decode_depth(z, dec)
             depth = dec.view(N, 1, H, W)
         else:
@@ -513,7 +517,7 @@ class RollingDepthPipeline:
         # ----------------- outputs (:345-353, D2H boundary; pinned, async, one sync)
         # input_rgb = frames / 2 + 0.5 in f16 as the reference computes it on the host (x/2 is exact,
         # the +0.5 rounds identically), evaluated on the device before the copy
-        rgb = input_frames[0].to(self.device, F16) / 2.0 + 0.5
+        rgb = input_frames[0].to(self.device, self.dtype) / 2.0 + 0.5
         outs = [self._to_host_async(t, d2h) for t in (rgb, depth, coaligned)]
         d2h.synchronize()
         return RollingDepthOutput(input_rgb=outs[0], depth_pred=outs[1], snippet_ls=snip_host,

@@ -156,11 +156,11 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     if f1 > f0:
         mine = pipe.encode_rgb(mine_frames.to(dev))
     else:
-        mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=F16, device=dev)
+        mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=pipe.dtype, device=dev)
     rgb_latent = _all_gather_rows(mine, N, world, group)
     if init_noise is None:
         g = torch.Generator(device=dev).manual_seed(0)
-        init_noise = torch.randn((1, 4, h, w), device=dev, dtype=F16, generator=g)
+        init_noise = torch.randn((1, 4, h, w), device=dev, dtype=pipe.dtype, generator=g)
     noise = pipe._noise_nhwc(init_noise, h, w)
     # 2. my snippets (compact: row r of dilation d is global snippet subsets[d][r])
     counts = [len(pipe.get_snippet_indice(0, [0], N, snippet_len, d, d, 1)) for d in dil]
@@ -187,28 +187,28 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     assert seq_len == N
     scales, trans, hist, ws = aligner.optimize_prepared(xs, strides, N)
     sums = K.aligner_merge_partial([r if r.shape[0] else None for r in rows], k0, counts, scales, trans, strides,
-                                   snippet_len, N, H * W, shift, x_f32=False)
+                                   snippet_len, N, H * W, shift, x_f32=pipe.dtype == F32)
     my_sums = _reduce_scatter_rows(sums, world, group)
     merged = K.aligner_merge_finish(my_sums, counts, strides, snippet_len, f0) if f1 > f0 else my_sums
-    d = merged.to(F16).float().contiguous()  # merge_scaled_triplets returns the snippets' dtype
+    d = merged.to(pipe.dtype).float().contiguous()  # merge_scaled_triplets returns the snippets' dtype
     mm_d = K.minmax(d) if d.numel() else torch.tensor([float("inf"), float("-inf")], device=dev)
     gmm = _all_reduce_minmax(mm_d, group)
     if d.numel():
         K.renormalize_(d, gmm)
-    coaligned = d.to(F16).view(f1 - f0, 1, H, W)
+    coaligned = d.to(pipe.dtype).view(f1 - f0, 1, H, W)
     del ws
     # 4. refine
     if refine_step > 0:
         if f1 > f0:
             dlat_mine = pipe.encode_rgb(coaligned.expand(-1, 3, -1, -1))
         else:
-            dlat_mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=F16, device=dev)
+            dlat_mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=pipe.dtype, device=dev)
         dlat = _all_gather_rows(dlat_mine, N, world, group)
         new = pipe.refine(rgb_latent, dlat, noise, refine_step, refine_snippet_len, refine_start_dilation,
                           group=group)
         if record is not None:
             record["refined_latent"] = new
-        depth = torch.empty((f1 - f0, H, W, 1), dtype=F16, device=dev)
+        depth = torch.empty((f1 - f0, H, W, 1), dtype=pipe.dtype, device=dev)
         if f1 > f0:
             z = K.ddim_combine(new[f0:f1, ..., :4], new[f0:f1, ..., :4], 1.0 / pipe.depth_latent_scale_factor, 0.0,
                                1.0, 4, 8)
@@ -228,6 +228,6 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
         out.depth_pred = pipe._to_host_async(depth, d2h)
         out.depth_coaligned = pipe._to_host_async(coaligned, d2h) if refine_step > 0 else out.depth_pred
         if f1 > f0:
-            out.input_rgb = pipe._to_host_async(mine_frames.to(dev, F16) / 2.0 + 0.5, d2h)
+            out.input_rgb = pipe._to_host_async(mine_frames.to(dev, pipe.dtype) / 2.0 + 0.5, d2h)
         d2h.synchronize()
     return out

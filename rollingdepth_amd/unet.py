@@ -40,10 +40,10 @@ def _sinusoid(t: int, dim: int, flip: bool, shift: float) -> np.ndarray:
 
 
 class _Lin:
-    def __init__(self, sd, key, dev, bias=True):
+    def __init__(self, sd, key, dev, bias=True, dtype=F16):
         w = sd[key + ".weight"]
         self.n, self.k = w.shape
-        self.w = K.pack_linear(w, dev)
+        self.w = K.pack_linear(w, dev, dtype)
         self.b = sd[key + ".bias"].to(dev, F32) if bias and key + ".bias" in sd else None
 
     def __call__(self, x, out=None, residual=None, silu=False, gn=False):
@@ -51,11 +51,11 @@ class _Lin:
 
 
 class _Conv:
-    def __init__(self, sd, key, dev, stride=1, pad=1):
+    def __init__(self, sd, key, dev, stride=1, pad=1, dtype=F16):
         w = sd[key + ".weight"]
         self.cout, self.cin, self.k, _ = w.shape
         self.cin_pad = K.pad_channels(self.cin)
-        self.w = K.pack_conv(w, dev, self.cin_pad)
+        self.w = K.pack_conv(w, dev, self.cin_pad, dtype)
         self.b = sd[key + ".bias"].to(dev, F32) if key + ".bias" in sd else None
         self.stride, self.pad = stride, pad
 
@@ -80,12 +80,13 @@ class _Norm:
 class Resnet:
     """ResnetBlock2D (resnet.py:189, forward :320-373)."""
 
-    def __init__(self, sd, p, dev, groups, eps, temb_slot=None):
+    def __init__(self, sd, p, dev, groups, eps, temb_slot=None, dtype=F16):
         self.n1 = _Norm(sd, p + ".norm1", dev)
-        self.c1 = _Conv(sd, p + ".conv1", dev)
+        self.c1 = _Conv(sd, p + ".conv1", dev, dtype=dtype)
         self.n2 = _Norm(sd, p + ".norm2", dev)
-        self.c2 = _Conv(sd, p + ".conv2", dev)
-        self.sc = _Conv(sd, p + ".conv_shortcut", dev, pad=0) if p + ".conv_shortcut.weight" in sd else None
+        self.c2 = _Conv(sd, p + ".conv2", dev, dtype=dtype)
+        self.sc = _Conv(sd, p + ".conv_shortcut", dev, pad=0, dtype=dtype) if p + ".conv_shortcut.weight" in sd \
+            else None
         self.groups, self.eps = groups, eps
         self.temb_slot = temb_slot  # (offset, width) into the concatenated time projections
 
@@ -103,33 +104,35 @@ class Transformer:
     """Transformer2DModel (use_linear_projection) + BasicTransformerBlock with the modified
     cross-frame attn1 (num_view fold) and attn2 against the constant context."""
 
-    def __init__(self, sd, p, dev, heads, groups):
+    def __init__(self, sd, p, dev, heads, groups, dtype=F16):
         self.heads, self.groups = heads, groups
         self.norm = _Norm(sd, p + ".norm", dev)
-        self.proj_in = _Lin(sd, p + ".proj_in", dev)
-        self.proj_out = _Lin(sd, p + ".proj_out", dev)
+        self.proj_in = _Lin(sd, p + ".proj_in", dev, dtype=dtype)
+        self.proj_out = _Lin(sd, p + ".proj_out", dev, dtype=dtype)
         q = p + ".transformer_blocks.0"
         self.ln1 = _Norm(sd, q + ".norm1", dev)
         self.ln2 = _Norm(sd, q + ".norm2", dev)
         self.ln3 = _Norm(sd, q + ".norm3", dev)
         wqkv = torch.cat([sd[f"{q}.attn1.to_{n}.weight"] for n in ("q", "k", "v")], 0)
         self.c = wqkv.shape[1]
-        self.qkv = K.pack_linear(wqkv, dev)
-        self.o1 = _Lin(sd, q + ".attn1.to_out.0", dev)
-        self.q2 = _Lin(sd, q + ".attn2.to_q", dev, bias=False)
-        self.k2 = _Lin(sd, q + ".attn2.to_k", dev, bias=False)
-        self.v2 = _Lin(sd, q + ".attn2.to_v", dev, bias=False)
-        self.o2 = _Lin(sd, q + ".attn2.to_out.0", dev)
+        self.qkv = K.pack_linear(wqkv, dev, dtype)
+        self.o1 = _Lin(sd, q + ".attn1.to_out.0", dev, dtype=dtype)
+        self.q2 = _Lin(sd, q + ".attn2.to_q", dev, bias=False, dtype=dtype)
+        self.k2 = _Lin(sd, q + ".attn2.to_k", dev, bias=False, dtype=dtype)
+        self.v2 = _Lin(sd, q + ".attn2.to_v", dev, bias=False, dtype=dtype)
+        self.o2 = _Lin(sd, q + ".attn2.to_out.0", dev, dtype=dtype)
         wp, bp = K.geglu_permute(sd[q + ".ff.net.0.proj.weight"], sd[q + ".ff.net.0.proj.bias"])
-        self.ff1_w = K.pack_linear(wp, dev)
+        self.ff1_w = K.pack_linear(wp, dev, dtype)
         self.ff1_b = bp.to(dev, F32)
-        self.ff2 = _Lin(sd, q + ".ff.net.2", dev)
+        self.ff2 = _Lin(sd, q + ".ff.net.2", dev, dtype=dtype)
         self._ctx_key = None
         # f16-rounded to_q / to_out weights for the two-token attn2 fold (set_context), kept only where
         # the folded [H, C] w / u tables fit the kernel's LDS (2·H·C·4 B ≤ 64 KiB, H ≤ 16: C ≤ 640 at d = 64)
+        # (f16 path only: the f32 path runs LN → q GEMM → attention → out GEMM in f32)
         self._pair = None
         self._pair_w = None
-        if 2 * heads * self.c * 4 <= 64 * 1024 and heads <= 16 and os.environ.get("RDMI_ATTN2_PAIR", "1") != "0":
+        if dtype == F16 and 2 * heads * self.c * 4 <= 64 * 1024 and heads <= 16 and \
+                os.environ.get("RDMI_ATTN2_PAIR", "1") != "0":
             self._pair_w = (sd[q + ".attn2.to_q.weight"].half().float().to(dev),
                             sd[q + ".attn2.to_out.0.weight"].half().float().to(dev),
                             sd.get(q + ".attn2.to_out.0.bias", torch.zeros(self.c)).float().to(dev))
@@ -182,9 +185,11 @@ class Transformer:
 class UNet:
     """Native UNet2DConditionModel (SD2 family: CrossAttnDown* + Down, mid CrossAttn, Up + CrossAttnUp*)."""
 
-    def __init__(self, cfg: dict, sd: Dict[str, torch.Tensor], device):
+    def __init__(self, cfg: dict, sd: Dict[str, torch.Tensor], device, dtype=F16):
         dev = torch.device(device)
-        self.cfg, self.dev = cfg, dev
+        if dtype not in (F16, F32):
+            raise NotImplementedError(f"UNet storage dtype {dtype} (f16 or f32)")
+        self.cfg, self.dev, self.dtype = cfg, dev, dtype
         g, eps = cfg["norm_num_groups"], cfg["norm_eps"]
         heads = unet_heads(cfg)
         ch = cfg["block_out_channels"]
@@ -192,9 +197,9 @@ class UNet:
         self.ch, self.L = ch, L
         self.in_ch = cfg["in_channels"]
         self.out_ch = cfg["out_channels"]
-        self.conv_in = _Conv(sd, "conv_in", dev)
-        self.t1 = _Lin(sd, "time_embedding.linear_1", dev)
-        self.t2 = _Lin(sd, "time_embedding.linear_2", dev)
+        self.conv_in = _Conv(sd, "conv_in", dev, dtype=dtype)
+        self.t1 = _Lin(sd, "time_embedding.linear_1", dev, dtype=dtype)
+        self.t2 = _Lin(sd, "time_embedding.linear_2", dev, dtype=dtype)
         # concatenated time_emb_proj of every resnet
         tp_w, tp_b, off = [], [], 0
         slots = {}
@@ -206,13 +211,13 @@ class UNet:
                 tp_b.append(sd[p + ".time_emb_proj.bias"])
                 slots[p] = (off, w.shape[0])
                 off += w.shape[0]
-        self.tp_w = K.pack_linear(torch.cat(tp_w, 0), dev)
+        self.tp_w = K.pack_linear(torch.cat(tp_w, 0), dev, dtype)
         self.tp_b = torch.cat(tp_b, 0).to(dev, F32)
         self.tp_k = tp_w[0].shape[1]
         self._temb_cache = {}
 
         def R(p):
-            return Resnet(sd, p, dev, g, eps, slots.get(p))
+            return Resnet(sd, p, dev, g, eps, slots.get(p), dtype=dtype)
 
         self.down = []
         for i, bt in enumerate(cfg["down_block_types"]):
@@ -220,12 +225,12 @@ class UNet:
             for j in range(L):
                 blk["res"].append(R(f"down_blocks.{i}.resnets.{j}"))
                 if bt == "CrossAttnDownBlock2D":
-                    blk["attn"].append(Transformer(sd, f"down_blocks.{i}.attentions.{j}", dev, heads[i], g))
+                    blk["attn"].append(Transformer(sd, f"down_blocks.{i}.attentions.{j}", dev, heads[i], g, dtype))
             if i < len(ch) - 1:
-                blk["ds"] = _Conv(sd, f"down_blocks.{i}.downsamplers.0.conv", dev, stride=2, pad=1)
+                blk["ds"] = _Conv(sd, f"down_blocks.{i}.downsamplers.0.conv", dev, stride=2, pad=1, dtype=dtype)
             self.down.append(blk)
         self.mid_res = [R("mid_block.resnets.0"), R("mid_block.resnets.1")]
-        self.mid_attn = Transformer(sd, "mid_block.attentions.0", dev, heads[-1], g)
+        self.mid_attn = Transformer(sd, "mid_block.attentions.0", dev, heads[-1], g, dtype)
         rheads = list(reversed(heads))
         self.up = []
         for i, bt in enumerate(cfg["up_block_types"]):
@@ -233,12 +238,12 @@ class UNet:
             for j in range(L + 1):
                 blk["res"].append(R(f"up_blocks.{i}.resnets.{j}"))
                 if bt == "CrossAttnUpBlock2D":
-                    blk["attn"].append(Transformer(sd, f"up_blocks.{i}.attentions.{j}", dev, rheads[i], g))
+                    blk["attn"].append(Transformer(sd, f"up_blocks.{i}.attentions.{j}", dev, rheads[i], g, dtype))
             if i < len(ch) - 1:
-                blk["us"] = _Conv(sd, f"up_blocks.{i}.upsamplers.0.conv", dev)
+                blk["us"] = _Conv(sd, f"up_blocks.{i}.upsamplers.0.conv", dev, dtype=dtype)
             self.up.append(blk)
         self.norm_out = _Norm(sd, "conv_norm_out", dev)
-        self.conv_out = _Conv(sd, "conv_out", dev)
+        self.conv_out = _Conv(sd, "conv_out", dev, dtype=dtype)
         self.groups, self.eps = g, eps
         self.transformers = [t for b in self.down for t in b["attn"]] + [self.mid_attn] + \
                             [t for b in self.up for t in b["attn"]]
@@ -251,7 +256,7 @@ class UNet:
         if e is not None:
             return e
         s = _sinusoid(int(t), self.ch[0], self.cfg.get("flip_sin_to_cos", True), self.cfg.get("freq_shift", 0))
-        x = torch.from_numpy(s).to(self.dev, F16).view(1, -1)
+        x = torch.from_numpy(s).to(self.dev, self.dtype).view(1, -1)
         h = K.gemm(x, self.t1.w, self.t1.k, bias=self.t1.b, silu=True)
         emb = K.gemm(h, self.t2.w, self.t2.k, bias=self.t2.b, silu=True)  # silu(temb) feeds every proj
         proj = K.gemm(emb, self.tp_w, self.tp_k, bias=self.tp_b, out_f32=True)

@@ -25,10 +25,10 @@ LATENT_SCALE = 0.18215
 
 
 class _FoldedConv(_Conv):
-    def __init__(self, w: torch.Tensor, b: torch.Tensor, dev, stride=1, pad=1):
+    def __init__(self, w: torch.Tensor, b: torch.Tensor, dev, stride=1, pad=1, dtype=F16):
         self.cout, self.cin, self.k, _ = w.shape
         self.cin_pad = K.pad_channels(self.cin)
-        self.w = K.pack_conv(w, dev, self.cin_pad)
+        self.w = K.pack_conv(w, dev, self.cin_pad, dtype)
         self.b = b.to(dev, F32)
         self.stride, self.pad = stride, pad
 
@@ -37,14 +37,14 @@ class VaeAttention:
     """Mid-block Attention (unet_2d_blocks.py:680-697; AttnProcessor2_0 4-D path): GroupNorm →
     fused biased QKV GEMM → f32 scores GEMM → row softmax → GEMM with Vᵀ → to_out + residual."""
 
-    def __init__(self, sd, p, dev, groups):
+    def __init__(self, sd, p, dev, groups, dtype=F16):
         self.norm = _Norm(sd, p + ".group_norm", dev)
         self.c = sd[p + ".to_q.weight"].shape[0]
         w = torch.cat([sd[f"{p}.to_{n}.weight"] for n in ("q", "k", "v")], 0)
         b = torch.cat([sd[f"{p}.to_{n}.bias"] for n in ("q", "k", "v")], 0)
-        self.qkv_w = K.pack_linear(w, dev)
+        self.qkv_w = K.pack_linear(w, dev, dtype)
         self.qkv_b = b.to(dev, F32)
-        self.out = _Lin(sd, p + ".to_out.0", dev)
+        self.out = _Lin(sd, p + ".to_out.0", dev, dtype=dtype)
         self.groups = groups
 
     def __call__(self, x):
@@ -59,9 +59,11 @@ class VaeAttention:
 
 
 class VAE:
-    def __init__(self, cfg: dict, sd: Dict[str, torch.Tensor], device):
+    def __init__(self, cfg: dict, sd: Dict[str, torch.Tensor], device, dtype=F16):
         dev = torch.device(device)
-        self.cfg, self.dev = cfg, dev
+        if dtype not in (F16, F32):
+            raise NotImplementedError(f"VAE storage dtype {dtype} (f16 or f32)")
+        self.cfg, self.dev, self.dtype = cfg, dev, dtype
         g = cfg["norm_num_groups"]
         eps = 1e-6
         ch = cfg["block_out_channels"]
@@ -73,40 +75,40 @@ class VAE:
         self.lat_pad = K.pad_channels(lat)
 
         def R(p):
-            return Resnet(sd, p, dev, g, eps)
+            return Resnet(sd, p, dev, g, eps, dtype=dtype)
 
         # encoder
-        self.e_in = _Conv(sd, "encoder.conv_in", dev)
+        self.e_in = _Conv(sd, "encoder.conv_in", dev, dtype=dtype)
         self.e_down = []
         for i in range(len(ch)):
             res = [R(f"encoder.down_blocks.{i}.resnets.{j}") for j in range(L)]
-            ds = _Conv(sd, f"encoder.down_blocks.{i}.downsamplers.0.conv", dev, stride=2, pad=0) \
+            ds = _Conv(sd, f"encoder.down_blocks.{i}.downsamplers.0.conv", dev, stride=2, pad=0, dtype=dtype) \
                 if i < len(ch) - 1 else None
             self.e_down.append((res, ds))
         self.e_mid = [R("encoder.mid_block.resnets.0"), R("encoder.mid_block.resnets.1")]
-        self.e_attn = VaeAttention(sd, "encoder.mid_block.attentions.0", dev, g)
+        self.e_attn = VaeAttention(sd, "encoder.mid_block.attentions.0", dev, g, dtype)
         self.e_norm = _Norm(sd, "encoder.conv_norm_out", dev)
         wq = sd["quant_conv.weight"][:lat, :, 0, 0]
         bq = sd["quant_conv.bias"][:lat]
         wo, bo = sd["encoder.conv_out.weight"], sd["encoder.conv_out.bias"]
         wf = torch.einsum("oc,cikj->oikj", wq.double(), wo.double()).float()
         bf = (wq.double() @ bo.double() + bq.double()).float()
-        self.e_out = _FoldedConv(wf * LATENT_SCALE, bf * LATENT_SCALE, dev)
+        self.e_out = _FoldedConv(wf * LATENT_SCALE, bf * LATENT_SCALE, dev, dtype=dtype)
         # decoder
-        self.post_quant = _Conv(sd, "post_quant_conv", dev, pad=0)
-        self.d_in = _Conv(sd, "decoder.conv_in", dev)
+        self.post_quant = _Conv(sd, "post_quant_conv", dev, pad=0, dtype=dtype)
+        self.d_in = _Conv(sd, "decoder.conv_in", dev, dtype=dtype)
         self.d_mid = [R("decoder.mid_block.resnets.0"), R("decoder.mid_block.resnets.1")]
-        self.d_attn = VaeAttention(sd, "decoder.mid_block.attentions.0", dev, g)
+        self.d_attn = VaeAttention(sd, "decoder.mid_block.attentions.0", dev, g, dtype)
         self.d_up = []
         for i in range(len(ch)):
             res = [R(f"decoder.up_blocks.{i}.resnets.{j}") for j in range(L + 1)]
-            us = _Conv(sd, f"decoder.up_blocks.{i}.upsamplers.0.conv", dev) if i < len(ch) - 1 else None
+            us = _Conv(sd, f"decoder.up_blocks.{i}.upsamplers.0.conv", dev, dtype=dtype) if i < len(ch) - 1 else None
             self.d_up.append((res, us))
         self.d_norm = _Norm(sd, "decoder.conv_norm_out", dev)
         wd, bd = sd["decoder.conv_out.weight"], sd["decoder.conv_out.bias"]
         wm = wd.double().mean(0, keepdim=True).float()  # [1, C, 3, 3]
         bm = bd.double().mean(0, keepdim=True).float()
-        self.d_out = _FoldedConv(wm, bm, dev)
+        self.d_out = _FoldedConv(wm, bm, dev, dtype=dtype)
         # the same folded conv as the fused GroupNorm+SiLU+conv head's [tap][C] f32 weights
         self.d_w9 = wm[0].permute(1, 2, 0).reshape(9, -1).contiguous().to(dev, F32)
         self.d_b = float(bm[0])
@@ -140,7 +142,7 @@ class VAE:
         h = self.e_mid[1](h)
         h = K.groupnorm(h, self.e_norm.g, self.e_norm.b, self.groups, 1e-6, silu=True)
         if out is None:
-            out = torch.zeros((B, h.shape[1], h.shape[2], self.lat_pad), dtype=F16, device=x.device)
+            out = torch.zeros((B, h.shape[1], h.shape[2], self.lat_pad), dtype=self.dtype, device=x.device)
         self.e_out(h, out=out)
         return out
 
@@ -149,7 +151,7 @@ class VAE:
         """z: NHWC f16 [B, h, w, lat_pad] holding latent/0.18215 (zero padded) → depth [B, H, W, 1]
         = mean over the decoder's RGB outputs."""
         B, hh, ww, _ = z.shape
-        h = torch.zeros((B, hh, ww, self.d_in.cin_pad), dtype=F16, device=z.device)
+        h = torch.zeros((B, hh, ww, self.d_in.cin_pad), dtype=self.dtype, device=z.device)
         self.post_quant(z, out=h)
         h = self.d_in(h, gn=True)
         h = self.d_mid[0](h)
