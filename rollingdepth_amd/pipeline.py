@@ -119,10 +119,16 @@ class RollingDepthPipeline:
         unet = UNet(ucfg, _load_state_dict(os.path.join(path, "unet")), device, dtype)
         vae = VAE(vcfg, _load_state_dict(os.path.join(path, "vae")), device, dtype)
         pipe = cls(unet, vae, DDIMScheduler.from_config(scfg))
-        emb = os.path.join(path, "empty_text_embed.safetensors")
-        if os.path.exists(emb):
-            from safetensors.torch import load_file
-            pipe.empty_text_embed = load_file(emb)["embed"]
+        if os.path.isdir(os.path.join(path, "text_encoder")) and os.path.isdir(os.path.join(path, "tokenizer")):
+            # encode_empty_text (rollingdepth_pipeline.py:178-191), once at load: the only use of
+            # text_encoder / tokenizer on the depth path (text_encoder.py)
+            from .text_encoder import empty_text_embedding
+            pipe.empty_text_embed = empty_text_embedding(path, dtype)
+        else:
+            emb = os.path.join(path, "empty_text_embed.safetensors")
+            if os.path.exists(emb):
+                from safetensors.torch import load_file
+                pipe.empty_text_embed = load_file(emb)["embed"]
         return pipe
 
     @classmethod
@@ -179,14 +185,15 @@ class RollingDepthPipeline:
         self._xformers_requested = False
 
     def encode_empty_text(self):
-        """rollingdepth_pipeline.py:178-191 — needs the CLIP text encoder; the build caches the
-        constant [1, 2, 1024] embedding instead (set `empty_text_embed`)."""
+        """rollingdepth_pipeline.py:178-191.  from_pretrained computes the constant embedding from the
+        checkpoint's text_encoder/ + tokenizer/ (text_encoder.py); with a transformers tokenizer and
+        text encoder handed to the constructor, they are run here as the reference runs them."""
         if self.text_encoder is None or self.tokenizer is None:
             raise RuntimeError("empty_text_embed not set and no text encoder available")
         ids = self.tokenizer("", padding="do_not_pad", max_length=self.tokenizer.model_max_length, truncation=True,
                              return_tensors="pt").input_ids
         with torch.no_grad():
-            self.empty_text_embed = self.text_encoder(ids)[0].float()
+            self.empty_text_embed = self.text_encoder(ids)[0].to(self.dtype)
 
     # ------------------------------------------------------------------ reference helpers
     @staticmethod

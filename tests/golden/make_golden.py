@@ -88,8 +88,41 @@ def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step
     return out, rec
 
 
-def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, refine_step=0, refine_start=6):
+TINY_CLIP = dict(vocab_size=30, hidden_size=96, intermediate_size=192, num_hidden_layers=2, num_attention_heads=4,
+                 max_position_embeddings=77, hidden_act="gelu", layer_norm_eps=1e-5, bos_token_id=0, eos_token_id=1,
+                 pad_token_id=1)
+TINY_VOCAB = {"<|startoftext|>": 0, "<|endoftext|>": 1, **{c: 2 + i for i, c in enumerate("abcdefghijklmn")},
+              **{c + "</w>": 16 + i for i, c in enumerate("abcdefghijklmn")}}
+
+
+def attach_clip(P, pipe):
+    """A transformers CLIPTokenizer + CLIPTextModel (tiny config, weights synthesised per key like the
+    UNet/VAE) on the reference pipeline, so forward() runs the reference's encode_empty_text."""
+    import tempfile
+
+    from transformers import CLIPTextConfig, CLIPTextModel, CLIPTokenizer
+
+    from rollingdepth_amd import text_encoder as TE
+
+    d = tempfile.mkdtemp()
+    json.dump(TINY_VOCAB, open(os.path.join(d, "vocab.json"), "w"))
+    open(os.path.join(d, "merges.txt"), "w").write("#version: 0.2\n")
+    tk = CLIPTokenizer(os.path.join(d, "vocab.json"), os.path.join(d, "merges.txt"), model_max_length=77)
+    cfg = CLIPTextConfig(**TINY_CLIP)
+    te = CLIPTextModel(cfg).eval()
+    syn = W.synth_state_dict(TE.text_encoder_param_shapes(TINY_CLIP), 0)
+    own = set(te.state_dict())
+    te.load_state_dict({(k if k in own else k[len("text_model."):]): v for k, v in syn.items()}, strict=True)
+    pipe.register_modules(text_encoder=te, tokenizer=tk)
+    pipe.empty_text_embed = None
+    return pipe
+
+
+def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, refine_step=0, refine_start=6,
+                     clip=False):
     pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
+    if clip:
+        attach_clip(P, pipe)
     h, w = frames.shape[-2] // C.vae_downscale(vcfg), frames.shape[-1] // C.vae_downscale(vcfg)
     noise = torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(1))
     out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign, refine_step, refine_start)
@@ -108,6 +141,8 @@ def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, 
     meta = {"dilations_in": list(dilations), "dilations_used": rec["dilations_used"], "cap_dilation": cap,
             "unet": ucfg, "vae": vcfg, "scheduler": C.RD_SCHEDULER, "coalign": coalign or {},
             "refine_step": refine_step, "refine_start_dilation": refine_start}
+    if clip:  # the context above is the reference's encode_empty_text output
+        meta.update(text_encoder=TINY_CLIP, tokenizer_vocab=TINY_VOCAB, text_encoder_seed=0)
     json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
     print(name, {k: tuple(v.shape) for k, v in t.items()})
 
@@ -283,7 +318,7 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", os.cpu_count() or 8)))
     P, A = _refload.load_reference()
-    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "sd2"]
+    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "clip", "sd2"]
     if "keys" in todo:
         keys_fixture()
     if "idx" in todo:
@@ -301,6 +336,9 @@ def main():
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_refine", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, refine_step=2,
                          refine_start=6)
+    if "clip" in todo:  # tiny pipeline whose empty-text context comes from the reference's CLIP path
+        frames = W.synth_frames(9, 32, 32, seed=0)
+        pipeline_fixture(P, "tiny_clip_pipeline", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, clip=True)
     if "sd2" in todo and not a.skip_sd2:
         frames = W.synth_frames(3, 256, 256, seed=0)
         pipeline_fixture(P, "sd2_256", C.SD2_UNET, C.SD2_VAE, frames, [1], False)

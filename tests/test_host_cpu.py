@@ -125,3 +125,40 @@ def test_shard_partition_covers_every_snippet_once(counts, world):
     assert seen == flat_snippets(counts)
     sizes = [hi - lo for lo, hi in chunk_bounds(sum(counts), world)]
     assert max(sizes) - min(s for s in sizes if s) <= max(1, max(sizes))
+
+
+def test_empty_text_embedding_vs_transformers_and_reference(tmp_path):
+    """encode_empty_text restated (rollingdepth_amd/text_encoder.py): tokenizer("") → [BOS, EOS] and the
+    CLIP text transformer on those two tokens — against transformers' CLIPTokenizer + CLIPTextModel
+    (the reference's own classes, rollingdepth_pipeline.py:178-191) on the same synthesised weights,
+    and against the context the reference pipeline computed for the tiny_clip_pipeline fixture."""
+    import json
+
+    from safetensors.torch import load_file
+
+    from rollingdepth_amd import text_encoder as TE
+    from tests.ckpt_util import write_text_encoder
+
+    meta = json.load(open(os.path.join(ROOT, "tests", "golden", "tiny_clip_pipeline.json")))
+    ref_ctx = load_file(os.path.join(ROOT, "tests", "golden", "tiny_clip_pipeline.safetensors"))["context"]
+    write_text_encoder(str(tmp_path), meta["text_encoder"], meta["tokenizer_vocab"], meta["text_encoder_seed"])
+    got = TE.empty_text_embedding(str(tmp_path))
+    assert got.shape == ref_ctx.shape == (1, 2, 96)
+    assert (got - ref_ctx).abs().max().item() < 1e-5
+    transformers = pytest.importorskip("transformers")
+    tk = transformers.CLIPTokenizer.from_pretrained(str(tmp_path / "tokenizer"))
+    ids = tk("", padding="do_not_pad", max_length=tk.model_max_length, truncation=True, return_tensors="pt").input_ids
+    assert ids.tolist() == [list(TE.special_token_ids(str(tmp_path / "tokenizer")))]
+    # SD2-sized text tower (1024 wide, 23 layers, OpenCLIP ViT-H's gelu) on synthesised weights
+    cfg = dict(meta["text_encoder"], hidden_size=1024, intermediate_size=4096, num_hidden_layers=23,
+               num_attention_heads=16)
+    big = tmp_path / "sd2"
+    write_text_encoder(str(big), cfg, meta["tokenizer_vocab"], 3)
+    m = transformers.CLIPTextModel(transformers.CLIPTextConfig(**cfg)).eval()
+    sd = load_file(str(big / "text_encoder" / "model.safetensors"))
+    own = set(m.state_dict())
+    m.load_state_dict({(k if k in own else k[len("text_model."):]): v for k, v in sd.items()}, strict=True)
+    with torch.no_grad():
+        want = m(ids)[0]
+    got = TE.empty_text_embedding(str(big))
+    assert (got - want).abs().max().item() < 2e-5 * max(1.0, want.abs().max().item())

@@ -319,3 +319,44 @@ def test_full_size_batching_invariance():
     assert torch.isfinite(a).all() and torch.isfinite(b).all()
     d = (a - b).abs()
     assert d.mean().item() < 1e-3 and d.max().item() < 5e-2 * (b.abs().max().item() + 1e-6), (d.mean(), d.max())
+
+
+def test_run_video_drop_in_sequence(tmp_path):
+    """run_video.py:523-585 as written, against a diffusers-format checkpoint directory written from
+    synthesised weights (model_index.json, unet/, vae/, scheduler/, text_encoder/, tokenizer/):
+    from_pretrained(path, torch_dtype) → enable_xformers_memory_efficient_attention() → .to(device)
+    → pipe(input_fg_video_path=…, input_bg_video_path=…, <the CLI's keyword set>) → R/G/B_pred.
+    The empty-text context comes from the checkpoint's CLIP text encoder (text_encoder.py), and the
+    outputs are checked against the reference pipeline that ran its own encode_empty_text
+    (tiny_clip_pipeline fixture).  Frames enter as a tensor (PyAV is absent; video_io.py) and the
+    fixture's init noise is injected (the reference draws it from its device RNG)."""
+    from rollingdepth_amd.pipeline import RollingDepthPipeline
+    from tests.ckpt_util import write_checkpoint
+
+    t = load_file(os.path.join(G, "tiny_clip_pipeline.safetensors"))
+    meta = json.load(open(os.path.join(G, "tiny_clip_pipeline.json")))
+    write_checkpoint(str(tmp_path), meta["unet"], meta["vae"], meta["scheduler"], meta["text_encoder"],
+                     meta["tokenizer_vocab"], meta["text_encoder_seed"])
+    dtype = torch.float16
+    pipe = RollingDepthPipeline.from_pretrained(str(tmp_path), torch_dtype=dtype)
+    try:
+        pipe.enable_xformers_memory_efficient_attention()
+    except ImportError:
+        pass
+    pipe = pipe.to(torch.device("cuda"))
+    assert pipe.dtype == dtype
+    assert (pipe.empty_text_embed.float().cpu() - t["context"]).abs().max().item() <= 2e-3 * t["context"].abs().max()
+    generator = torch.Generator(device="cuda").manual_seed(0)
+    out = pipe(input_fg_video_path=t["frames"], input_bg_video_path="unused.mp4", start_frame=0, frame_count=0,
+               processing_res=32, resample_method="BILINEAR", dilations=list(meta["dilations_in"]),
+               cap_dilation=meta["cap_dilation"], snippet_lengths=[3], init_infer_steps=[1], strides=[1],
+               coalign_kwargs=None, refine_step=0, refine_snippet_len=3, refine_start_dilation=6,
+               generator=generator, verbose=False, max_vae_bs=4, restore_res=False, unload_snippet=False,
+               init_noise=t["init_noise"])
+    combined = torch.cat((out.R_pred, out.G_pred, out.B_pred), dim=1)  # run_video.py:606
+    assert combined.shape == (t["frames"].shape[0], 3, *t["frames"].shape[-2:])
+    assert torch.equal(out.R_pred, out.depth_pred.float() * 0.5 + 0.5)
+    assert len(out.aligned_snippet_pred_ls[0]) > 1
+    m, mx, _ = _stats(out.depth_pred, t["depth_pred"])
+    print(f"run_video drop-in: depth L1 {m:.2e} max {mx:.2e}")
+    assert m <= DEPTH_L1
