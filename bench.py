@@ -143,9 +143,7 @@ def _validate(pipe, frames_dev, noise, dil0, snippet0, depth_host, coalign) -> d
         return info
     # re-run the first snippet of dilation 1 alone: frames 0..2, 1 snippet per UNet call, 3-frame encode
     lat = pipe.encode_rgb(frames_dev[:3])
-    from rollingdepth_amd import kernels as K
-
-    nz = K.nchw_to_nhwc(noise.to(pipe.device), 8)
+    nz = pipe._noise_nhwc(noise, lat.shape[1], lat.shape[2])
     sb = pipe.snippet_batch
     pipe.snippet_batch = 1
     try:
@@ -199,10 +197,6 @@ def main():
     pr = dict(PRESETS[a.preset])
     res = a.res or pr["res"]
     dil0 = [int(x) for x in a.dilations.split(",")] if a.dilations else list(pr["dilations"])
-    if pr["dtype"] != "f16":
-        print(f"bench.py: preset {a.preset} computes in {pr['dtype']}; this build's bench path runs f16 only "
-              f"(a narrower-precision number would not be the reference's arithmetic)", file=sys.stderr)
-        sys.exit(2)
     if a.frames_total is not None or (a.frames is None and pr["frames_total"] is not None):
         N = a.frames_total or pr["frames_total"]
         scaling = "strong"
@@ -221,14 +215,15 @@ def main():
     from rollingdepth_amd.pipeline import RollingDepthPipeline
     from rollingdepth_amd.shard import chunk_bounds, sharded_forward
 
-    pipe = RollingDepthPipeline.from_synthetic(C.SD2_UNET, C.SD2_VAE, C.RD_SCHEDULER, device=dev)
+    tdt = torch.float32 if pr["dtype"] == "f32" else torch.float16
+    pipe = RollingDepthPipeline.from_synthetic(C.SD2_UNET, C.SD2_VAE, C.RD_SCHEDULER, device=dev, torch_dtype=tdt)
     pipe.snippet_batch = a.snippet_batch
     pipe.vae_batch = a.vae_batch
     if world > 1:  # each rank materialises only its own chunk of the synthetic video
         lo, hi = chunk_bounds(N, world)[rank]
-        frames = W.synth_frames(N, res, res, seed=0, first=lo, count=hi - lo).to(dev, torch.float16)
+        frames = W.synth_frames(N, res, res, seed=0, first=lo, count=hi - lo).to(dev, tdt)
     else:
-        frames = W.synth_frames(N, res, res, seed=0)[None].to(dev, torch.float16)
+        frames = W.synth_frames(N, res, res, seed=0)[None].to(dev, tdt)
     noise = W.synth_noise(res // 8, res // 8).to(dev)
     coalign = {"num_iterations": a.aligner_iters}
     refine = pr["refine"]
@@ -291,16 +286,17 @@ def main():
         dom = max(prof, key=lambda k: prof[k]["ms"])
         p = prof[dom]
         ach = _fam(dom)
-        peak = PEAK_F16_TFLOPS
+        peak = PEAK_F32_TFLOPS if dom.endswith("_f32") else PEAK_F16_TFLOPS
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": None, "launches": p["n"],
                 "avg_launch_us": round(p["ms"] * 1e3 / max(p["n"], 1), 2),
                 "per_kernel": {k: {"tflops": round(_fam(k), 1), "ms": round(v["ms"], 1), "launches": v["n"]}
                                for k, v in prof.items()}}
-        if "attention_fwd" in prof:
-            att = _fam("attention_fwd")
-            roof["attention"] = {"achieved": round(att, 1), "peak": peak, "unit": "TFLOP/s",
-                                 "frac": round(att / peak, 4)}
+        for an, apk in (("attention_fwd", PEAK_F16_TFLOPS), ("attention_fwd_f32", PEAK_F32_TFLOPS)):
+            if an in prof:
+                att = _fam(an)
+                roof["attention"] = {"kernel": an, "achieved": round(att, 1), "peak": apk, "unit": "TFLOP/s",
+                                     "frac": round(att / apk, 4)}
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
         cpu = _cpu_baseline(a.cpu_768_runs)

@@ -255,7 +255,9 @@ int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream);
 int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int H, int W, int border,
                          int factor, const float* shift, float* out, void* stream);
 /* merge_scaled_triplets (:231-262): full-resolution snippets per dilation xf_d [n_d][w][HW]
- * (f16 or f32 per x_f32; the min shift read from shift[0] is applied first, in that dtype),
+ * (x_f32 = 1: f32 snippets; 0: f16 snippets in the reference's f16 arithmetic; 2: f16 snippets with
+ * the shift and s·x+t in f32 — no intermediate f16 rounding; the min shift read from shift[0] is
+ * applied first),
  * s/t f32 → out [seq_len][HW] f32 (s·x+t rounded through the snippet dtype exactly where the
  * reference computes in it; the per-frame mean is accumulated in f32). */
 int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,

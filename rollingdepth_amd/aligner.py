@@ -56,7 +56,10 @@ class DepthAligner:
                                 self.lmda3, self.depth_loss_weight, self.loss_scale, self.num_iterations, hist)
         return scales, trans, hist, ws
 
-    def run(self, snippet_ls: List[torch.Tensor], dilations: List[int]):
+    def run(self, snippet_ls: List[torch.Tensor], dilations: List[int], merged_f32: bool = False):
+        """depth_aligner.py:68-120.  merged_f32=True (the pipeline's internal use): the merge of f16
+        snippets runs in f32 arithmetic and is returned in f32, without the reference's f16 roundings
+        of s·x+t and of the merged map (RollingDepthPipeline.merge_f32)."""
         dev = torch.device(self.device)
         snippet_ls = [s.to(dev) for s in snippet_ls]
         lengths = [s.shape[1] for s in snippet_ls]
@@ -77,8 +80,8 @@ class DepthAligner:
         xs = self.prepare(flat, shift)
         strides = [g + 1 for g in gaps]
         scales, trans, hist, ws = self.optimize_prepared(xs, strides, seq_len)
-        merged = K.aligner_merge(flat, scales, trans, strides, seq_len, shift)
-        merged = merged.to(dtype)[:, None]
+        merged = K.aligner_merge(flat, scales, trans, strides, seq_len, shift, f32_arith=merged_f32)
+        merged = (merged if merged_f32 else merged.to(dtype))[:, None]
         loss_ls = [tuple(r) for r in hist[: self.num_iterations].tolist()]
         del ws
         return (merged, [s.view(-1, 1, 1) for s in scales], [t.view(-1, 1, 1) for t in trans], loss_ls)

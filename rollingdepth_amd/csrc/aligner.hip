@@ -293,8 +293,11 @@ __global__ void merge_k(MergeP p) {
         if (k < p.k0[d] || k >= p.k0[d] + p.nloc[d]) continue;
         long off = ((long)(k - p.k0[d]) * p.w + j) * p.HW + px;
         float a;
-        if (p.xf32) {
+        if (p.xf32 == 1) {
           float xs = ((const float*)p.x[d])[off] - sh;
+          a = addrn(mulrn(xs, p.s[d][k]), p.t[d][k]);
+        } else if (p.xf32 == 2) {  // f16 snippets, f32 arithmetic (no intermediate f16 rounding)
+          float xs = (float)((const f16*)p.x[d])[off] - sh;
           a = addrn(mulrn(xs, p.s[d][k]), p.t[d][k]);
         } else {
           f16 xs = (f16)((float)((const f16*)p.x[d])[off] - sh);

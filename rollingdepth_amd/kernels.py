@@ -162,7 +162,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     part = _gn_part(out, M, N) if (gn and batch == 1 and not geglu and not out_f32) else None
     if part is not None:
         g.gn_part, g.gn_ld = part.data_ptr(), part.stride(0)
-    with _Timed("implicit_gemm", 2.0 * M * N * k * batch, f"gemm M={M} N={N} K={k} b={batch}"):
+    with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * M * N * k * batch,
+                f"gemm M={M} N={N} K={k} b={batch}"):
         check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
     _gn_attach(out, part)
     return out
@@ -293,7 +294,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
         a.gn_part, a.gn_ld = _gn_slot
-    with _Timed("implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin,
+    with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin,
                 f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}"):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
     if _gn_slot is None:
@@ -705,8 +706,10 @@ def aligner_optimize(xs: Sequence[torch.Tensor], scales: Sequence[torch.Tensor],
     return ws  # keep alive until the stream has consumed it
 
 
-def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: int, shift: torch.Tensor) -> torch.Tensor:
-    """xf[d] [n_d, w, H, W] (f16/f32) → [seq_len, H, W] f32."""
+def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: int, shift: torch.Tensor,
+                  f32_arith: bool = False) -> torch.Tensor:
+    """xf[d] [n_d, w, H, W] (f16/f32) → [seq_len, H, W] f32.  f16 snippets are merged in the
+    reference's f16 arithmetic unless f32_arith (rdmi.h rdmi_aligner_merge x_f32 = 2)."""
     nd = len(xf)
     n_, w, H, W = xf[0].shape
     out = torch.empty((seq_len, H, W), dtype=F32, device=xf[0].device)
@@ -715,13 +718,14 @@ def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: i
     tp = (C.c_void_p * nd)(*[t.data_ptr() for t in trans])
     nn = (C.c_int * nd)(*[x.shape[0] for x in xf])
     stv = (C.c_int * nd)(*list(strides))
-    check(lib.rdmi_aligner_merge(nd, xp, int(xf[0].dtype == F32), sp, tp, nn, stv, w, seq_len, H * W,
+    mode = 1 if xf[0].dtype == F32 else (2 if f32_arith else 0)
+    check(lib.rdmi_aligner_merge(nd, xp, mode, sp, tp, nn, stv, w, seq_len, H * W,
                                  shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge")
     return out
 
 
 def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int], n: Sequence[int], scales, trans,
-                          strides, w: int, seq_len: int, HW: int, shift: torch.Tensor, x_f32: bool,
+                          strides, w: int, seq_len: int, HW: int, shift: torch.Tensor, x_f32,
                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sharded merge, rank-local half: xf[d] [nloc_d, w, H, W] = global snippets k0[d] .. of dilation
     d (None / 0 rows when the rank owns none) → f32 [seq_len, HW] per-frame sums of s·x+t."""

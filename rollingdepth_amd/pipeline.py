@@ -86,6 +86,13 @@ def _balanced(n: int, cap: int) -> List[Tuple[int, int]]:
     return out
 
 
+def _resolve(d: torch.device) -> torch.device:
+    """An index-less "cuda" names the current device."""
+    if d.type == "cuda" and d.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 def _contiguous_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     """Rank's share of `total` equal-cost units: W contiguous ranges of ceil(total/W)."""
     c = (total + world - 1) // world
@@ -105,6 +112,9 @@ class RollingDepthPipeline:
         self.vae_batch = 75      # max frames per VAE encode / decode call (memory-capped: _vae_chunks)
         self._dev = unet.dev
         self._group = None  # torch.distributed group for snippet-parallel forward (enable_snippet_parallel)
+        # merge_scaled_triplets of f16 snippets in f32 arithmetic, merged map kept f32 until the output
+        # (the reference's fp16 run rounds s·x+t and the merged map to f16 before the renormalisation)
+        self.merge_f32 = os.environ.get("RDMI_MERGE_F32", "0") == "1"
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -161,10 +171,9 @@ class RollingDepthPipeline:
                 if a != self.dtype:
                     raise NotImplementedError(f"pipeline built for {self.dtype}; rebuild it with torch_dtype={a}")
                 continue
-            d = torch.device(a)
-            idx = d.index if d.index is not None else (torch.cuda.current_device() if d.type == "cuda" else None)
-            if d.type != self._dev.type or idx != self._dev.index:
-                raise NotImplementedError(f"pipeline lives on {self._dev}; construct it on {d} instead")
+            d, mine = _resolve(torch.device(a)), _resolve(self._dev)
+            if d != mine:
+                raise NotImplementedError(f"pipeline lives on {mine}; construct it on {d} instead")
         return self
 
     def enable_snippet_parallel(self, group=None):
@@ -388,15 +397,15 @@ class RollingDepthPipeline:
             if world == 1:
                 new = K.snippet_average(preds, stride, N)
             else:
-                import torch.distributed as dist
+                from .shard import _all_reduce
                 sums = K.snippet_accumulate(preds, lo, stride, N)
-                dist.all_reduce(sums, group=group)
+                _all_reduce(sums, group=group)
                 new = K.snippet_finish(sums, len(idx), snippet_len, stride, (h, w), 8, dtype=self.dtype)
         return new
 
     # ------------------------------------------------------------------ entry points
     @torch.no_grad()
-    def __call__(self, input_video_path, start_frame: int = 0, frame_count: int = 0, processing_res: int = 1024,
+    def __call__(self, input_video_path=None, start_frame: int = 0, frame_count: int = 0, processing_res: int = 1024,
                  resample_method: str = "BILINEAR", dilations: List[int] = [1, 25], cap_dilation: bool = True,
                  snippet_lengths: List[int] = [3], init_infer_steps: List[int] = [1], strides: List[int] = [1],
                  coalign_kwargs: Union[Dict, None] = None, refine_step: int = 0, refine_snippet_len: int = 3,
@@ -502,7 +511,7 @@ class RollingDepthPipeline:
         # ----------------- co-alignment + renormalisation (:306-318)
         aligner = DepthAligner(device=self.device, verbose=verbose, **(coalign_kwargs or {}))
         merged, scales, trans, hist = aligner.run([s.view(s.shape[0], s.shape[1], 1, H, W) for s in snippets],
-                                                  dilations)
+                                                  dilations, merged_f32=self.merge_f32)
         d = merged.float().contiguous()
         K.renormalize_(d, K.minmax(d))
         coaligned = d.to(self.dtype)

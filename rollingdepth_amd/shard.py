@@ -60,6 +60,30 @@ def rank_subsets(counts: Sequence[int], world: int, rank: int) -> List[List[int]
     return sub
 
 
+def _via_host(group, t: torch.Tensor) -> bool:
+    """gloo has no device transport: device tensors are staged through host memory (tests that run
+    several ranks on one GPU, or CPU ranks); RCCL moves device memory directly over xGMI."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
+    if _via_host(group, inp):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def _all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
+    if _via_host(group, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
 def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) -> torch.Tensor:
     """All-gather the rows of chunk_bounds(total, world)[rank] from every rank → [total, ...]."""
     c = (total + world - 1) // world
@@ -67,7 +91,7 @@ def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) ->
         pad = torch.zeros((c - local.shape[0], *local.shape[1:]), dtype=local.dtype, device=local.device)
         local = torch.cat([local, pad])
     out = torch.empty((c * world, *local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    _gather_into(out, local.contiguous(), group)
     return out[:total]
 
 
@@ -79,7 +103,12 @@ def _reduce_scatter_rows(full: torch.Tensor, world: int, group=None) -> torch.Te
         full = torch.cat([full, torch.zeros((c * world - total, *full.shape[1:]), dtype=full.dtype,
                                             device=full.device)])
     out = torch.empty((c, *full.shape[1:]), dtype=full.dtype, device=full.device)
-    dist.reduce_scatter_tensor(out, full.contiguous(), group=group)
+    if _via_host(group, full):
+        o = out.cpu()
+        dist.reduce_scatter_tensor(o, full.contiguous().cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.reduce_scatter_tensor(out, full.contiguous(), group=group)
     rank = dist.get_rank(group)
     lo, hi = chunk_bounds(total, world)[rank]
     return out[:hi - lo]
@@ -104,7 +133,7 @@ def gather_rows_by_dilation(local: Sequence[torch.Tensor], counts: Sequence[int]
 def _all_reduce_minmax(mm: torch.Tensor, group=None) -> torch.Tensor:
     """[min, max] f32 → the global [min, max] (one MIN all-reduce of [min, −max])."""
     t = torch.stack([mm[0], -mm[1]])
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    _all_reduce(t, dist.ReduceOp.MIN, group)
     return torch.stack([t[0], -t[1]])
 
 
@@ -187,10 +216,12 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     assert seq_len == N
     scales, trans, hist, ws = aligner.optimize_prepared(xs, strides, N)
     sums = K.aligner_merge_partial([r if r.shape[0] else None for r in rows], k0, counts, scales, trans, strides,
-                                   snippet_len, N, H * W, shift, x_f32=pipe.dtype == F32)
+                                   snippet_len, N, H * W, shift,
+                                   x_f32=1 if pipe.dtype == F32 else (2 if pipe.merge_f32 else 0))
     my_sums = _reduce_scatter_rows(sums, world, group)
     merged = K.aligner_merge_finish(my_sums, counts, strides, snippet_len, f0) if f1 > f0 else my_sums
-    d = merged.to(pipe.dtype).float().contiguous()  # merge_scaled_triplets returns the snippets' dtype
+    # merge_scaled_triplets returns the snippets' dtype (unless the pipeline merges in f32)
+    d = (merged if pipe.merge_f32 else merged.to(pipe.dtype).float()).contiguous()
     mm_d = K.minmax(d) if d.numel() else torch.tensor([float("inf"), float("-inf")], device=dev)
     gmm = _all_reduce_minmax(mm_d, group)
     if d.numel():

@@ -1,0 +1,66 @@
+"""Targets for rocprofv3 PMC passes (tools/pmc_round.sh): one shape, a few launches.
+
+    python tools/traffic_probe.py --what copy|conv|attn [--iters 3]
+
+copy: a 1 GiB f16 device copy (reads 1 GiB, writes 1 GiB) — the known-bytes calibration of
+      FETCH_SIZE / WRITE_SIZE for 16-B-per-lane streaming (the guide's ½ correction is checked here);
+conv: the dominant conv of the metric config — VAE decoder 768² 128→128, 3×3, with the fused
+      GroupNorm+SiLU input, the residual add and the GroupNorm-moment epilogue (ResnetBlock2D.conv2 of
+      up_blocks.3), batch 8 (algorithmic bytes printed);
+attn: level-0 cross-frame attention at 768² (B = 8 snippets, S = 27 648, H = 5)."""
+import argparse
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from rollingdepth_amd import kernels as K  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--what", default="conv")
+ap.add_argument("--iters", type=int, default=3)
+ap.add_argument("--batch", type=int, default=8)
+a = ap.parse_args()
+torch.manual_seed(0)
+if a.what == "copy":
+    n = 1 << 29  # halves: 1 GiB
+    x = torch.randn(n // 1024, 1024, device="cuda").half()
+    y = torch.empty_like(x)
+    fn = lambda: y.copy_(x)  # noqa: E731
+    print(f"algorithmic: read {n * 2} B, write {n * 2} B per launch")
+elif a.what == "conv":
+    B, H, W, C = a.batch, 768, 768, 128
+    x = torch.randn(B, H, W, C, device="cuda").half()
+    res = torch.randn(B, H, W, C, device="cuda").half()
+    gm = 1 + 0.1 * torch.randn(C, device="cuda")
+    bt = 0.1 * torch.randn(C, device="cuda")
+    w = K.pack_conv(torch.randn(C, C, 3, 3) / math.sqrt(C * 9), "cuda", C)
+    b = 0.02 * torch.randn(C, device="cuda")
+    mr = K.groupnorm_stats(x, 32, 1e-6)
+    out = torch.empty(B, H, W, C, device="cuda", dtype=torch.float16)
+
+    def fn():
+        K.conv2d(x, w, C, 3, bias=b, residual=res, out=out, gn=True, in_gn=(mr, gm, bt, 32, True))
+
+    act = B * H * W * C * 2
+    print(f"algorithmic: read {2 * act + w.numel() * 2} B (input + residual + weights), write {act} B "
+          f"(+ GroupNorm moments {C // 4 * B * H * W // 32 * 8} B); {2.0 * B * H * W * C * C * 9:.4e} FLOP")
+else:
+    B, S, H = a.batch, 27648, 5
+    C = H * 64
+    qkv = torch.randn(B, S, 3 * C, device="cuda").half()
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    out = torch.empty(B, S, C, device="cuda", dtype=torch.float16)
+    fn = lambda: K.attention(q, k, v, H, out=out)  # noqa: E731
+    print(f"algorithmic: {4.0 * B * H * S * S * 64:.4e} FLOP; read {3 * B * S * C * 2} B, write {B * S * C * 2} B")
+for _ in range(a.iters):
+    fn()
+torch.cuda.synchronize()
+s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+s.record()
+fn()
+e.record()
+torch.cuda.synchronize()
+print(f"done: {s.elapsed_time(e) * 1e3:.1f} us per launch (event-timed, last launch)")
