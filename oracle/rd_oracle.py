@@ -544,3 +544,30 @@ def pipeline_forward(usd, ucfg, vsd, vcfg, scfg, frames: torch.Tensor, init_nois
             record.update(refined_latent=new)
         d = decode_depth(vsd, vcfg, new, max_vae_bs)
     return d
+
+
+# ----------------------------------------------------------------------------- colourisation
+def colorize_index(depth: np.ndarray, mn, mx, n: int) -> np.ndarray:
+    """Colormap table index per pixel: colorize_depth's normalisation (src/util/colorize.py:26, numpy
+    arithmetic in the depth's dtype) followed by matplotlib Colormap.__call__'s float → index rule
+    (x·N, x == N → N−1, truncating cast; NaN → the 'bad' entry N + 2)."""
+    dt = depth.dtype
+    x = ((depth - dt.type(mn)) / (dt.type(mx) - dt.type(mn))).clip(0, 1)
+    x = x * dt.type(n)
+    x[x == n] = n - 1
+    idx = x.astype(np.int64)
+    idx[np.isnan(x)] = n + 2
+    return idx
+
+
+def colorize_depth_multi_thread(depth: np.ndarray, valid_mask=None, color_map: str = "Spectral") -> np.ndarray:
+    """src/util/colorize.py:41-93 (single-threaded restatement): [N,1,H,W] → uint8 [N,H,W,3]."""
+    import matplotlib
+
+    d = depth.squeeze(1)
+    v = d if valid_mask is None else d[valid_mask.reshape(d.shape).astype(bool)]
+    cm = matplotlib.colormaps[color_map]
+    if not cm._isinit:
+        cm._init()
+    lut = (cm._lut[:, :3] * 255).astype(np.uint8)
+    return lut[colorize_index(d, v.min(), v.max(), cm.N)]

@@ -89,6 +89,7 @@ _SIGS = {
     "rdmi_snippet_average": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
     "rdmi_snippet_accumulate": (i32, [vp, i32, i32, i32, i32, i32, i32, i64, i32, i32, vp, vp]),
     "rdmi_snippet_finish": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
+    "rdmi_colorize": (i32, [vp, i32, i64, vp, vp, i32, vp, vp, vp]),
     "rdmi_minmax": (i32, [vp, i32, i64, vp, vp, vp]),
     "rdmi_renormalize_f32": (i32, [vp, i64, vp, vp]),
     "rdmi_aligner_workspace": (i64, [C.POINTER(AlignerArgs)]),

@@ -189,6 +189,39 @@ __global__ void snippet_finish_k(const float* __restrict__ sum, int n, int w, in
   }
 }
 
+// colorize_depth (src/util/colorize.py:12-66): per pixel, normalise by (min, max) in the depth's own
+// dtype as numpy does ((d - mn) / (mx - mn), clip to [0, 1]), index a matplotlib colormap the way
+// Colormap.__call__ does for floats (x·N, x == N → N−1, truncating int cast; NaN → the "bad" entry
+// N + 2), and write the 8-bit RGB the reference gets from (lut·255).astype(uint8) (host-built table).
+__device__ __forceinline__ float rnd(const f16*, float v) { return (float)(f16)v; }
+__device__ __forceinline__ float rnd(const float*, float v) { return v; }
+
+template <typename T>
+__global__ void colorize_k(const T* __restrict__ d, long n, const T* __restrict__ mm, const unsigned char* __restrict__ lut,
+                           int N, unsigned char* __restrict__ out, int* __restrict__ idx_out) {
+  const float mn = (float)mm[0], rng = rnd(d, (float)mm[1] - (float)mm[0]);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float v = (float)d[i];
+    int idx;
+    if (v != v) {
+      idx = N + 2;
+    } else {
+      float x = rnd(d, __fdiv_rn(rnd(d, v - mn), rng));
+      x = fminf(fmaxf(x, 0.f), 1.f);
+      x = rnd(d, x * (float)N);
+      if (x == (float)N) x = (float)(N - 1);
+      idx = (int)x;
+    }
+    if (idx_out) {
+      idx_out[i] = idx;
+      continue;
+    }
+    out[3 * i] = lut[3 * idx];
+    out[3 * i + 1] = lut[3 * idx + 1];
+    out[3 * i + 2] = lut[3 * idx + 2];
+  }
+}
+
 // 16-B vector loads (8 halves / 4 floats per lane and step), scalar tail; min/max are
 // order-independent, so the result is exact whatever the split.
 __global__ __launch_bounds__(256) void minmax_partial(const void* __restrict__ x, int xf32, long n,
@@ -407,4 +440,16 @@ extern "C" int rdmi_snippet_finish(const float* sum, int n, int w, int stride, i
     hipLaunchKernelGGL(snippet_finish_k<f16>, dim3((unsigned)gx, N), dim3(256), 0, (hipStream_t)stream, sum, n, w,
                        stride, P, C, ld, (f16*)out);
   return rdmi::check_launch("snippet_finish");
+}
+
+extern "C" int rdmi_colorize(const void* depth, int dtype, long n, const void* minmax, const unsigned char* lut,
+                             int lut_n, unsigned char* rgb, int* index, void* stream) {
+  RDMI_REQUIRE(depth && minmax && n > 0 && lut_n > 0 && ((lut && rgb) || index), RDMI_E_ARG, "colorize: bad args");
+  if (dtype == RDMI_F32)
+    hipLaunchKernelGGL(colorize_k<float>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const float*)depth, n,
+                       (const float*)minmax, lut, lut_n, rgb, index);
+  else
+    hipLaunchKernelGGL(colorize_k<f16>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const f16*)depth, n,
+                       (const f16*)minmax, lut, lut_n, rgb, index);
+  return rdmi::check_launch("colorize");
 }

@@ -112,9 +112,11 @@ class RollingDepthPipeline:
         self.vae_batch = 75      # max frames per VAE encode / decode call (memory-capped: _vae_chunks)
         self._dev = unet.dev
         self._group = None  # torch.distributed group for snippet-parallel forward (enable_snippet_parallel)
-        # merge_scaled_triplets of f16 snippets in f32 arithmetic, merged map kept f32 until the output
-        # (the reference's fp16 run rounds s·x+t and the merged map to f16 before the renormalisation)
-        self.merge_f32 = os.environ.get("RDMI_MERGE_F32", "0") == "1"
+        # merge_scaled_triplets of f16 snippets in f32 arithmetic, the merged map kept f32 through the
+        # renormalisation (the reference's fp16 run rounds s·x+t and the merged map to f16 first; those
+        # roundings of the extreme pixels rescale the whole renormalised map — tools/precision_probe.py:
+        # 768² depth L1 vs the fp32 reference 1.13e-3 → 7.6e-4).  RDMI_MERGE_F32=0: the fp16 roundings.
+        self.merge_f32 = os.environ.get("RDMI_MERGE_F32", "1") == "1"
 
     # ------------------------------------------------------------------ construction
     @classmethod

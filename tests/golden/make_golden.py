@@ -188,6 +188,33 @@ def compact_fixture(P, name, ucfg, vcfg, n, res, dilations, cap, depth_stride, r
     print(name, {k: tuple(v.shape) for k, v in t.items()}, flush=True)
 
 
+def colorize_fixture():
+    """src/util/colorize.py (the reference's visualisation) on random depth maps, f16 and f32, with and
+    without a valid mask; output uint8 / float bytes are the golden."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ref_colorize", "/root/reference/src/util/colorize.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    g = torch.Generator().manual_seed(11)
+    out = {}
+    d32 = (torch.randn(5, 1, 24, 32, generator=g) * 0.6).clamp(-1, 1)
+    d32[0, 0, 0, :4] = torch.tensor([-1.0, 1.0, 0.0, 0.5])
+    d16 = d32.half()
+    mask = (torch.rand(5, 1, 24, 32, generator=g) > 0.2)
+    for nm, d in (("f32", d32), ("f16", d16)):
+        out[f"depth_{nm}"] = d.clone()
+        out[f"rgb_{nm}"] = torch.from_numpy(mod.colorize_depth_multi_thread(d.numpy(), color_map="Spectral"))
+        out[f"rgb_{nm}_masked"] = torch.from_numpy(
+            mod.colorize_depth_multi_thread(d.numpy(), valid_mask=mask[:, 0].numpy(), color_map="Spectral"))
+        dn = d.numpy()[:, 0]
+        out[f"float_{nm}_Spectral_r"] = torch.from_numpy(
+            mod.colorize_depth(dn, float(dn.min()) * 0.9, float(dn.max()) * 0.8, cmap="Spectral_r").copy())
+    out["mask"] = mask
+    save_file({k: v.contiguous() for k, v in out.items()}, os.path.join(HERE, "colorize.safetensors"))
+    print("colorize", {k: tuple(v.shape) for k, v in out.items()})
+
+
 def attn_fixture():
     from diffusers.models.attention_processor import Attention, AttnProcessor2_0
 
@@ -318,7 +345,7 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", os.cpu_count() or 8)))
     P, A = _refload.load_reference()
-    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "clip", "sd2"]
+    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "clip", "colorize", "sd2"]
     if "keys" in todo:
         keys_fixture()
     if "idx" in todo:
@@ -336,6 +363,8 @@ def main():
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_refine", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, refine_step=2,
                          refine_start=6)
+    if "colorize" in todo:
+        colorize_fixture()
     if "clip" in todo:  # tiny pipeline whose empty-text context comes from the reference's CLIP path
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_clip_pipeline", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, clip=True)

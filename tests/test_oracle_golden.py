@@ -141,3 +141,16 @@ def test_tiny_refine_oracle_vs_reference():
 @pytest.mark.skipif(not os.path.exists(os.path.join(G, "sd2_256.safetensors")), reason="sd2 fixture not generated")
 def test_sd2_256_oracle_vs_reference():
     _pipeline_check("sd2_256", 1e-3, 1e-3)
+
+
+def test_colorize_oracle_vs_reference_golden():
+    """The colourisation restatement against src/util/colorize.py's own output (colorize.safetensors,
+    generated by running the reference module): bit-exact uint8, f16 and f32 depth, with a mask."""
+    from safetensors.torch import load_file
+
+    t = load_file(os.path.join(G, "colorize.safetensors"))
+    for nm in ("f32", "f16"):
+        d = t[f"depth_{nm}"].numpy()
+        assert np.array_equal(O.colorize_depth_multi_thread(d), t[f"rgb_{nm}"].numpy())
+        m = t["mask"].numpy()[:, 0]
+        assert np.array_equal(O.colorize_depth_multi_thread(d, m), t[f"rgb_{nm}_masked"].numpy())
