@@ -218,8 +218,9 @@ int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long 
 /* Depth colourisation (src/util/colorize.py:12-93, the CLI's visualisation): rgb [n][3] u8 =
  * lut[idx(d)] with idx as matplotlib's Colormap.__call__ computes it for the normalised depth
  * ((d - minmax[0]) / (minmax[1] - minmax[0]) clipped to [0, 1], evaluated in the depth's dtype),
- * lut [(lut_n + 3)][3] = (colormap table · 255) as uint8 incl. the under / over / bad entries.  minmax in
- * the depth's dtype.  index != NULL: write the table index per pixel instead (lut / rgb unused). */
+ * lut [(lut_n + 3)][3] = (colormap table · 255) as uint8 incl. the under / over / bad entries.  minmax =
+ * {min, max − min} in the depth's dtype (the range as the reference's numpy forms it).  index != NULL:
+ * write the table index per pixel instead (lut / rgb unused). */
 int rdmi_colorize(const void* depth, int dtype, long n, const void* minmax, const unsigned char* lut, int lut_n,
                   unsigned char* rgb, int* index, void* stream);
 /* Sharded refine averaging (the loop above split over ranks): sum [N][P][C] f32 =

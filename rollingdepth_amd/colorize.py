@@ -37,10 +37,15 @@ def _lut_u8(name: str, device):
     return _LUTS[key]
 
 
-def _launch(d: torch.Tensor, mm: torch.Tensor, name: str, index: bool) -> torch.Tensor:
+def _np_dtype(d: torch.Tensor):
+    return np.float16 if d.dtype == torch.float16 else np.float32
+
+
+def _launch(d: torch.Tensor, mn_rng, name: str, index: bool) -> torch.Tensor:
+    """mn_rng: (min, max − min) as numpy scalars of the depth's dtype."""
     lut, n = _lut_u8(name, d.device)
     d = d.contiguous()
-    mmd = mm.to(d.device, d.dtype).contiguous()
+    mmd = torch.from_numpy(np.array(mn_rng, dtype=_np_dtype(d))).to(d.device)
     if index:
         out = torch.empty(d.shape, dtype=torch.int32, device=d.device)
         rc = lib.rdmi_colorize(d.data_ptr(), K._dtype_code(d), d.numel(), mmd.data_ptr(), None, n, None,
@@ -72,8 +77,9 @@ def colorize_depth(depth: Union[np.ndarray, torch.Tensor], min_depth: float, max
     d = _as_device(depth, device)
     if d.dim() < 3:
         d = d[None]
-    mm = torch.tensor([min_depth, max_depth], dtype=d.dtype)
-    idx = _launch(d, mm, cmap, index=True).cpu().numpy()
+    # Python-float bounds: their difference is a Python float, rounded to the depth dtype by numpy
+    nt = _np_dtype(d)
+    idx = _launch(d, (nt(min_depth), nt(max_depth - min_depth)), cmap, index=True).cpu().numpy()
     return _cmap(cmap)._lut[idx][..., :3]
 
 
@@ -85,9 +91,10 @@ def colorize_depth_multi_thread(depth: Union[np.ndarray, torch.Tensor], valid_ma
     reference's signature; the whole video is one device launch."""
     d = _as_device(depth, device).squeeze(1)
     assert d.dim() == 3
+    nt = _np_dtype(d)
     if valid_mask is None:
-        mm = K.minmax(d)
+        mn, mx = (nt(v) for v in K.minmax(d).tolist())  # exact: min / max are values of the depth dtype
     else:  # the reference reduces the masked pixels with numpy on the host (colorize.py:54-59)
         v = d.cpu().numpy()[np.asarray(valid_mask).reshape(d.shape).astype(bool)]
-        mm = torch.tensor([v.min(), v.max()], dtype=d.dtype)
-    return _launch(d, mm, color_map, index=False).cpu().numpy()
+        mn, mx = v.min(), v.max()
+    return _launch(d, (mn, mx - mn), color_map, index=False).cpu().numpy()

@@ -199,7 +199,7 @@ __device__ __forceinline__ float rnd(const float*, float v) { return v; }
 template <typename T>
 __global__ void colorize_k(const T* __restrict__ d, long n, const T* __restrict__ mm, const unsigned char* __restrict__ lut,
                            int N, unsigned char* __restrict__ out, int* __restrict__ idx_out) {
-  const float mn = (float)mm[0], rng = rnd(d, (float)mm[1] - (float)mm[0]);
+  const float mn = (float)mm[0], rng = (float)mm[1];  // {min, max − min}, both as the caller's numpy computes them
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float v = (float)d[i];
     int idx;
