@@ -25,6 +25,9 @@ match the batched result within the north_star depth bound (mean |Δ| ≤ 1e-3).
 Extra JSON fields: `roofline` for the dominant kernel family by summed time (achieved = algorithmic
 FLOPs of every launch of that family in the timed steps ÷ their summed HIP-event durations, events
 recorded on the launch stream), with the fused attention reported beside it (`roofline.attention`);
+`roofline.traffic` = HBM bytes per launch of that family from the committed rocprofv3 PMC passes over
+one step of the same preset (profiles/bench_traffic.json, tools/pmc_bench.sh), beside the algorithmic
+bytes per launch (every operand read once, output written once) measured here;
 `cpu_baseline`: the CPU oracle (oracle/rd_oracle.py, fp32 PyTorch restatement of the reference
 pipeline, pinned to reference golden vectors) on this host — BASELINE configs[0] (3 frames 256²),
 median of 3 after a warm-up, plus one 3-frame 768² snippet.
@@ -128,17 +131,36 @@ def _relaunch(n: int) -> int:
     return subprocess.call(cmd)
 
 
-def _validate(pipe, frames_dev, noise, dil0, snippet0, depth_host, coalign) -> dict:
-    """Output checks after the timed steps; raises on failure."""
+def _pmc_traffic(preset: str, family: str):
+    """HBM bytes per launch of `family` from the committed PMC passes over this preset's bench step
+    (tools/pmc_bench.sh → tools/bench_traffic.py → profiles/bench_traffic.json), or None."""
+    f = os.path.join(ROOT, "profiles", "bench_traffic.json")
+    try:
+        ent = json.load(open(f))[preset]
+        fam = ent["families"][family]
+    except (OSError, KeyError, ValueError):
+        return None
+    return {"bytes_per_launch": fam["bytes_per_launch"], "source": ent["source"]}
+
+
+def _validate(pipe, frames_dev, noise, dil0, snippet0, depth_host, coaligned_host, whole=True) -> dict:
+    """Output checks after the timed steps; raises on failure.  The co-aligned depth is renormalised
+    to [-1, 1] (rollingdepth_pipeline.py:315-317); the refined depth_pred is a decoder output and is
+    not (:336-342), so only its finiteness is checked.  whole=False: a rank's frame range, which
+    need not reach both ends of the range."""
     import torch
 
     d = depth_host.float()
     if not torch.isfinite(d).all():
         raise RuntimeError("bench validation: depth_pred has non-finite values")
-    lo, hi = d.min().item(), d.max().item()
-    if lo < -1.0 - 1e-3 or hi > 1.0 + 1e-3:
-        raise RuntimeError(f"bench validation: depth_pred range [{lo}, {hi}] not within [-1, 1]")
-    info = {"depth_finite": True, "depth_range": [round(lo, 4), round(hi, 4)]}
+    c = coaligned_host.float()
+    if not torch.isfinite(c).all():
+        raise RuntimeError("bench validation: depth_coaligned has non-finite values")
+    lo, hi = c.min().item(), c.max().item()
+    if lo < -1.0 - 1e-3 or hi > 1.0 + 1e-3 or (whole and min(-lo, hi) < 1.0 - 1e-3):
+        raise RuntimeError(f"bench validation: depth_coaligned range [{lo}, {hi}] is not [-1, 1]")
+    info = {"depth_finite": True, "coaligned_range": [round(lo, 4), round(hi, 4)],
+            "depth_range": [round(d.min().item(), 4), round(d.max().item(), 4)]}
     if snippet0 is None:
         return info
     # re-run the first snippet of dilation 1 alone: frames 0..2, 1 snippet per UNet call, 3-frame encode
@@ -234,11 +256,13 @@ def main():
             so = sharded_forward(pipe, frames, list(dil0), pr["cap"], 3, coalign, init_noise=noise, num_frames=N,
                                  to_host=True, refine_step=refine)
             last["depth"] = so.depth_pred
+            last["coaligned"] = so.depth_coaligned
             last["snip0"] = so.snippet_rows[0][0] if rank == 0 and so.snippet_rows[0].shape[0] else None
             return
         out = pipe.forward(frames, list(dil0), pr["cap"], [3], [1], [1], coalign, refine, 3, 6, None, False, 4,
                            False, init_noise=noise)
         last["depth"] = out.depth_pred
+        last["coaligned"] = out.depth_coaligned
         last["snip0"] = out.snippet_ls[0][0]
 
     for _ in range(a.warmup):
@@ -265,7 +289,7 @@ def main():
         try:
             vframes = frames if world > 1 else frames[0]
             validation = _validate(pipe, vframes, noise, dil0, last["snip0"] if rank == 0 else None, last["depth"],
-                                   coalign)
+                                   last["coaligned"], whole=world == 1)
             ok = 1
         except Exception as e:  # noqa: BLE001 — reported, then non-zero exit
             print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
@@ -287,8 +311,11 @@ def main():
         p = prof[dom]
         ach = _fam(dom)
         peak = PEAK_F32_TFLOPS if dom.endswith("_f32") else PEAK_F16_TFLOPS
+        tr = _pmc_traffic(a.preset, dom)
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": None, "launches": p["n"],
+                "frac": round(ach / peak, 4), "traffic": tr and round(tr["bytes_per_launch"]),
+                "algorithmic_bytes_per_launch": round(p["bytes"] / max(p["n"], 1)),
+                "traffic_source": tr and tr["source"], "launches": p["n"],
                 "avg_launch_us": round(p["ms"] * 1e3 / max(p["n"], 1), 2),
                 "per_kernel": {k: {"tflops": round(_fam(k), 1), "ms": round(v["ms"], 1), "launches": v["n"]}
                                for k, v in prof.items()}}

@@ -39,8 +39,9 @@ def profile_stop():
     torch.cuda.synchronize()
     out = {}
     for name, recs in prof.items():
-        ms = sum(a.elapsed_time(b) for a, b, _ in recs)
-        out[name] = {"ms": ms, "flop": float(sum(f for _, _, f in recs)), "n": len(recs)}
+        ms = sum(a.elapsed_time(b) for a, b, _, _ in recs)
+        out[name] = {"ms": ms, "flop": float(sum(r[2] for r in recs)), "bytes": float(sum(r[3] for r in recs)),
+                     "n": len(recs)}
     return out
 
 
@@ -48,10 +49,11 @@ _PROF_SHAPES = os.environ.get("RDMI_PROF_SHAPES") == "1"  # key the timings by l
 
 
 class _Timed:
-    __slots__ = ("name", "flop", "ev")
+    """nbytes: the launch's algorithmic HBM bytes (every operand read once, the output written once)."""
+    __slots__ = ("name", "flop", "nbytes", "ev")
 
-    def __init__(self, name, flop, shape=None):
-        self.name, self.flop, self.ev = name, flop, None
+    def __init__(self, name, flop, shape=None, nbytes=0):
+        self.name, self.flop, self.nbytes, self.ev = name, flop, nbytes, None
         if _PROF_SHAPES and shape is not None:
             self.name = f"{name} {shape}"
 
@@ -65,7 +67,7 @@ class _Timed:
         if _PROF is not None and self.ev is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            _PROF.setdefault(self.name, []).append((self.ev, e, self.flop))
+            _PROF.setdefault(self.name, []).append((self.ev, e, self.flop, self.nbytes))
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -162,8 +164,12 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     part = _gn_part(out, M, N) if (gn and batch == 1 and not geglu and not out_f32) else None
     if part is not None:
         g.gn_part, g.gn_ld = part.data_ptr(), part.stride(0)
+    es = a.element_size()
+    nb = es * (batch * M * k + (batch if w.dim() == 3 else 1) * N * k) + out.element_size() * batch * M * NO
+    if residual is not None:
+        nb += es * batch * M * NO
     with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * M * N * k * batch,
-                f"gemm M={M} N={N} K={k} b={batch}"):
+                f"gemm M={M} N={N} K={k} b={batch}", nb):
         check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
     _gn_attach(out, part)
     return out
@@ -294,8 +300,11 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
         a.gn_part, a.gn_ld = _gn_slot
+    es = x.element_size()
+    nb = es * (x.numel() + cout * k * k * Cin + (2 if residual is not None else 1) * B * Ho * Wo * cout)
     with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin,
-                f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}"):
+                f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}",
+                nb):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
     if _gn_slot is None:
         _gn_attach(out, part)
@@ -402,7 +411,8 @@ def conv3x3_to1_gn(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, gro
     if out.numel() != B * H * W or not out.is_contiguous() or out.dtype != x.dtype:
         raise ValueError("conv3x3_to1_gn: out must be a contiguous [B, H, W, 1] tensor")
     ws = _workspace(lib.rdmi_conv3x3_to1_gn_workspace(B, H, W), x.device)
-    with _Timed("conv_head", 2.0 * 9 * C_ * B * H * W, f"head B={B} {H}x{W} {C_}->1"):
+    with _Timed("conv_head", 2.0 * 9 * C_ * B * H * W, f"head B={B} {H}x{W} {C_}->1",
+                x.element_size() * B * H * W * (C_ + 1)):
         check(lib.rdmi_conv3x3_to1_gn(x.data_ptr(), _dtype_code(x), B, H, W, C_, groups, mr.data_ptr(), gamma.data_ptr(),
                                       beta.data_ptr(), int(silu), w9.data_ptr(), float(bias), out.data_ptr(),
                                       ws.data_ptr(), _stream()), "rdmi_conv3x3_to1_gn")
@@ -436,7 +446,9 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
         out = torch.empty((B, Sq, HD), dtype=q.dtype, device=q.device)
     sc = 1.0 / math.sqrt(D) if scale is None else scale
     name = "attention_fwd" if q.dtype == F16 else "attention_fwd_f32"
-    with _Timed(name, 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}"):
+    es = q.element_size()
+    with _Timed(name, 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}",
+                es * B * heads * D * (2 * Sq + 2 * Sk)):
         check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
                                      q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
                                      v.stride(0), out.stride(0), sc, _dtype_code(q), _stream()), "rdmi_attention_fwd")

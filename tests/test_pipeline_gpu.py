@@ -118,12 +118,15 @@ def test_sd2_256_pipeline_vs_reference_golden():
     _check("sd2_256")
 
 
-def _run_compact(name, snippet_batch=25):
-    if not os.path.exists(os.path.join(G, name + ".safetensors")):
-        pytest.skip(f"fixture {name} not generated")
+def _run_compact(name, snippet_batch=25, dtype=torch.float16, lat=None, unet=None):
     """Large-resolution reference fixtures (make_golden.compact_fixture): frames re-synthesised
     (checksummed against the generator's), latents stored f16, first snippet per dilation, depth on
-    a [::s, ::s] lattice + whole-map mean / mean |x|."""
+    a [::s, ::s] lattice + whole-map mean / mean |x|.  lat / unet: (max, mean) relative bounds,
+    default the f16 path's."""
+    if not os.path.exists(os.path.join(G, name + ".safetensors")):
+        pytest.skip(f"fixture {name} not generated")
+    lat = lat or (LAT_MAX, LAT_MEAN)
+    unet = unet or (UNET_MAX, UNET_MEAN)
     from rollingdepth_amd import weights as W
     from rollingdepth_amd.pipeline import RollingDepthPipeline
 
@@ -132,29 +135,29 @@ def _run_compact(name, snippet_batch=25):
     frames = W.synth_frames(meta["n_frames"], meta["res"], meta["res"], seed=meta["frames_seed"])
     cs = torch.tensor([frames.double().sum().item(), frames.double().abs().sum().item()], dtype=torch.float64)
     assert torch.allclose(cs, t["frames_checksum"].double(), rtol=1e-6), "synth_frames drifted"
-    pipe = RollingDepthPipeline.from_synthetic(meta["unet"], meta["vae"], meta["scheduler"], device="cuda")
+    pipe = RollingDepthPipeline.from_synthetic(meta["unet"], meta["vae"], meta["scheduler"], device="cuda",
+                                               torch_dtype=dtype)
     pipe.snippet_batch = snippet_batch
     pipe.empty_text_embed = t["context"]
     rec = {}
     dil = list(meta["dilations_in"])
-    out = pipe.forward(frames[None], dil, meta["cap_dilation"], [3], [1], [1], None, meta["refine_step"], 3,
+    out = pipe.forward(frames[None].to(dtype), dil, meta["cap_dilation"], [3], [1], [1], None, meta["refine_step"], 3,
                        meta["refine_start_dilation"], None, False, 4, False, init_noise=t["init_noise"], record=rec)
     assert dil == meta["dilations_used"]
     s = meta["depth_stride"]
     F = _Fails()
-    _check_rel(name, "rgb_latent", _nchw(rec["rgb_latent"]), t["rgb_latent"], LAT_MAX, LAT_MEAN, F)
-    _check_rel(name, "unet_out_first", _nchw(rec["unet_out"][0][:3]), t["unet_out_first"], UNET_MAX, UNET_MEAN, F)
+    _check_rel(name, "rgb_latent", _nchw(rec["rgb_latent"]), t["rgb_latent"], *lat, F)
+    _check_rel(name, "unet_out_first", _nchw(rec["unet_out"][0][:3]), t["unet_out_first"], *unet, F)
     lat0 = [_nchw(b[:3]) for b in rec["snippet_latent"]]  # first batch of each dilation starts at snippet 0
     bi = 0
     for i in range(len(dil)):
-        _check_rel(name, f"snippet_latent_{i}_first", lat0[bi], t[f"snippet_latent_{i}_first"], UNET_MAX, UNET_MEAN,
-                   F)
+        _check_rel(name, f"snippet_latent_{i}_first", lat0[bi], t[f"snippet_latent_{i}_first"], *unet, F)
         bi += len(pipe._snippet_batches(out.snippet_ls[i].shape[0], 3, *rec["rgb_latent"].shape[1:3]))
         m, mx, r = _stats(out.snippet_ls[i][0, :, 0, ::s, ::s], t[f"snippet_{i}_first_sub"])
         print(f"{name} snippet_{i}[0] (decoded, lattice) L1 {m:.2e} max {mx:.2e}")
         F.check(m <= DEPTH_L1, f"snippet_{i}[0]", m)
     if meta["refine_step"] > 0:
-        _check_rel(name, "refined_latent", _nchw(rec["refined_latent"]), t["refined_latent"], UNET_MAX, UNET_MEAN, F)
+        _check_rel(name, "refined_latent", _nchw(rec["refined_latent"]), t["refined_latent"], *unet, F)
     m, mx, r = _stats(out.depth_coaligned[..., ::s, ::s], t["depth_coaligned_sub"])
     print(f"{name} coaligned L1 (lattice) {m:.2e} max {mx:.2e}")
     F.check(m <= DEPTH_L1, "coaligned", m)
@@ -183,6 +186,12 @@ def test_fast1024_snippet_vs_reference_golden():
 def test_full1024_refine_vs_reference_golden():
     """full preset: 1024², dilations [1,10,25] capped as the reference caps them, 10 refine steps."""
     _run_compact("full1024")
+
+
+def test_paper256_f16_vs_reference_golden():
+    """Paper preset shape (dilations [1, 10, 25] uncapped, refine 10) on 51 frames at 256², f16 path
+    against the reference's fp32 run."""
+    _run_compact("paper256")
 
 
 def test_snippet_batching_invariance():

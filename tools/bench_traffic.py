@@ -1,0 +1,76 @@
+"""HBM traffic per launch of bench.py's kernel families, from two rocprofv3 --pmc passes over one
+bench step (tools/pmc_bench.sh: FETCH_SIZE and WRITE_SIZE need separate passes).
+
+    python tools/bench_traffic.py --fetch gpurun_out/pmc_bench/fetch --write gpurun_out/pmc_bench/write \
+        --preset fast --source profiles/r02_pmc_bench_summary.txt --out profiles/bench_traffic.json
+
+Reading rules (MI355X_MICROARCH.md § HBM): FETCH_SIZE (KB) reports ½ of the bytes of 16-B-per-lane
+streaming reads, `buffer_load … lds` included — doubled here, checked on a known-bytes copy
+(profiles/r02_pmc_summary.txt, pass copy_fetch: 1 GiB copy → 524 300 KB); WRITE_SIZE (KB) is exact
+for 16-B streaming stores (copy_write: 1 048 576 KB).  Both count L2 → fabric requests, so Infinity-
+Cache (MALL) hits are included: the figure is an upper bound on HBM bytes.
+
+The families are the ones bench.py times (kernels._Timed): implicit_gemm = every f16 GEMM / conv
+engine, attention_fwd = the f16 flash kernel, and their _f32 twins."""
+import argparse
+import csv
+import json
+import os
+import re
+
+FAMILIES = [
+    ("implicit_gemm_f32", re.compile(r"gemm_f32_kernel")),
+    ("attention_fwd_f32", re.compile(r"attn_fwd_f32")),
+    ("implicit_gemm", re.compile(r"conv_halo_kernel|conv_halo_occ2_kernel|gemm_pp_kernel|gemm_occ2_kernel|gemm_kernel<")),
+    ("attention_fwd", re.compile(r"attn_fwd_d64")),
+]
+
+
+def family(name: str):
+    for fam, rx in FAMILIES:
+        if rx.search(name):
+            return fam
+    return None
+
+
+def load(d: str, counter: str):
+    out = {}
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if r["Counter_Name"] != counter:
+            continue
+        fam = family(r["Kernel_Name"])
+        if fam is None:
+            continue
+        e = out.setdefault(fam, [0.0, 0])
+        e[0] += float(r["Counter_Value"]) * 1024.0
+        e[1] += 1
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--preset", default="fast")
+    ap.add_argument("--source", default="")
+    ap.add_argument("--out", default="profiles/bench_traffic.json")
+    a = ap.parse_args()
+    f, w = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
+    res = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    fams = {}
+    for fam in sorted(set(f) | set(w)):
+        fb, fn = f.get(fam, (0.0, 0))
+        wb, wn = w.get(fam, (0.0, 0))
+        n = max(fn, wn)
+        fams[fam] = {"fetch_B_per_launch": 2.0 * fb / max(fn, 1), "write_B_per_launch": wb / max(wn, 1),
+                     "bytes_per_launch": 2.0 * fb / max(fn, 1) + wb / max(wn, 1), "launches": n}
+        print(f"{fam:20s} launches {n:6d}  fetch {2 * fb / max(fn, 1) / 1e6:10.2f} MB  "
+              f"write {wb / max(wn, 1) / 1e6:10.2f} MB per launch")
+    res[a.preset] = {"families": fams, "source": a.source,
+                     "rule": "FETCH_SIZE x2 (gfx950 16-B streaming reads), WRITE_SIZE x1; L2->fabric bytes, "
+                             "MALL hits included"}
+    json.dump(res, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
