@@ -47,6 +47,28 @@ def load(d: str, counter: str):
     return out
 
 
+def write_summary(fd: str, wd: str, path: str) -> None:
+    """Per-kernel totals of both passes (FETCH_SIZE raw and ×2, WRITE_SIZE), largest first."""
+    agg = {}
+    for d, cn in ((fd, "FETCH_SIZE"), (wd, "WRITE_SIZE")):
+        for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+            if r["Counter_Name"] != cn:
+                continue
+            n = r["Kernel_Name"].replace("(anonymous namespace)::", "").removeprefix("void ")
+            n = re.sub(r"\(.*", "", n)[:90] if "at::native" not in n else "torch: " + n.split("<")[0][:80]
+            e = agg.setdefault(n, {"FETCH_SIZE": [0.0, 0], "WRITE_SIZE": [0.0, 0]})
+            e[cn][0] += float(r["Counter_Value"]) * 1024.0
+            e[cn][1] += 1
+    rows = sorted(agg.items(), key=lambda kv: -(2 * kv[1]["FETCH_SIZE"][0] + kv[1]["WRITE_SIZE"][0]))
+    with open(path, "w") as f:
+        f.write("# rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, one bench step, per kernel (bytes; fetch x2 = gfx950 "
+                "16-B streaming correction)\n")
+        f.write(f"{'kernel':90s} {'launches':>8s} {'fetch_raw_B':>14s} {'fetch_x2_B':>14s} {'write_B':>14s}\n")
+        for n, e in rows:
+            f.write(f"{n:90s} {e['FETCH_SIZE'][1]:8d} {e['FETCH_SIZE'][0]:14.4e} {2 * e['FETCH_SIZE'][0]:14.4e} "
+                    f"{e['WRITE_SIZE'][0]:14.4e}\n")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
@@ -54,7 +76,10 @@ def main():
     ap.add_argument("--preset", default="fast")
     ap.add_argument("--source", default="")
     ap.add_argument("--out", default="profiles/bench_traffic.json")
+    ap.add_argument("--summary", default=None, help="also write a per-kernel table here")
     a = ap.parse_args()
+    if a.summary:
+        write_summary(a.fetch, a.write, a.summary)
     f, w = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     res = json.load(open(a.out)) if os.path.exists(a.out) else {}
     fams = {}
