@@ -10,6 +10,8 @@
 // (activations.py:113-123), f16 or f32 output.
 #include "common.h"
 
+#include <utility>
+
 namespace {
 
 constexpr int BK = 64;  // K per stage: 8 chunks of 8 halves (16 B) per tile row
@@ -34,6 +36,7 @@ struct GemmP {
   const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
   int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
   int gelu_exact;  // GEGLU through ocml erff instead of gelu_erf_fast (RDMI_GELU_EXACT=1, A/B)
+  int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
 };
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
@@ -1041,6 +1044,20 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
 }
 
+// Issue-order pins for conv_halo_occ2_kernel's pipelined K-tile (sched_group_barrier needs
+// constant operands): group ST = [its DS reads: A(ST+PD), and the second k half's B fragments at
+// ST = BPRE] then its RN MFMAs.
+template <int RN, int PD, int NS, int BPRE, int ST>
+__device__ __forceinline__ void occ2_sched_one() {
+  constexpr int nr = (ST == BPRE ? RN : 0) + (ST + PD < NS ? 1 : 0);
+  if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
+  __builtin_amdgcn_sched_group_barrier(0x008, RN, 0);
+}
+template <int RN, int PD, int NS, int BPRE, int... S>
+__device__ __forceinline__ void occ2_sched(std::integer_sequence<int, S...>) {
+  (occ2_sched_one<RN, PD, NS, BPRE, S>(), ...);
+}
+
 // Two-workgroups-per-CU halo conv for 128-channel output tiles (the VAE's 768² convs).  With
 // 128 output channels and Cin = 128 a tile has only 18 K-tiles, so the 8-wave single-workgroup
 // variant above pays its prologue and epilogue un-overlapped on every tile (≈7 µs of ≈27 µs:
@@ -1055,7 +1072,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
 // fragment reads and 64 MFMAs.  At a channel block's first tap the halo is refilled in place:
 // barrier (all reads of the previous block's halo done), DMA, wait, [GroupNorm+SiLU of the own
 // pieces], barrier.
-template <int MODE, bool GN>
+template <int MODE, bool GN, bool PIPE>
 __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   constexpr int BN = 128, BKP = 64, RM = 8, RN = 4;
   constexpr int HWD = 18, HPIX = HWD * HWD;
@@ -1214,25 +1231,55 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     if (u + 1 < nk) issueB(u + 1);
     const f16* lb = lds + HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
     const int xb = fr + dx + 2 * dy;
-    f16x8 af[2][RM], bf[2][RN];
+    auto readA = [&](int kh, int i) {
+      const f16* row = lds + ((wms * RM + i + dy) * HWD + dx) * BKP;
+      return *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
+    };
+    if constexpr (PIPE) {
+      // Software-pipelined fragment reads over the K-tile's 16 MFMA groups s = (kh, i): A(s+2) is
+      // read while group s's 4 MFMAs issue, the second k half's B fragments 3 groups ahead of their
+      // first use (≈44 live fragment registers instead of 96: with the f32 accumulators the
+      // all-reads-first form ran out of registers, and the compiler then serialised every A read
+      // behind lgkmcnt(0) in front of its MFMAs).  The sched_group_barrier sequence pins the issue
+      // order (the scheduler otherwise sinks each read to just before its use).
+      constexpr int NS = 2 * RM, PD = 2, BPRE = RM - 3;
+      f16x8 bfr[2][RN], ar[PD + 1];
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int off = kh ? off1 : off0;
+      for (int j = 0; j < RN; ++j) bfr[0][j] = *(const f16x8*)(lb + j * 16 * BKP + off0);
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+      for (int q = 0; q < PD; ++q) ar[q] = readA(q / RM, q % RM);
 #pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const f16* row = lds + ((wms * RM + i + dy) * HWD + dx) * BKP;
-        af[kh][i] = *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
-      }
-    }
+      for (int st = 0; st < NS; ++st) {
+        if (st == BPRE) {
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
+          for (int j = 0; j < RN; ++j) bfr[1][j] = *(const f16x8*)(lb + j * 16 * BKP + off1);
+        }
+        if (st + PD < NS) ar[(st + PD) % (PD + 1)] = readA((st + PD) / RM, (st + PD) % RM);
+        const int kh = st / RM, i = st % RM;
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[kh][j], ar[st % (PD + 1)], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, RN + PD, 0);
+      occ2_sched<RN, PD, NS, BPRE>(std::make_integer_sequence<int, NS>{});
+    } else {
+      f16x8 af[2][RM], bf[2][RN];
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int off = kh ? off1 : off0;
+#pragma unroll
+        for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+#pragma unroll
+        for (int i = 0; i < RM; ++i) af[kh][i] = readA(kh, i);
+      }
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
+    }
   }
   store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
 }
@@ -1563,6 +1610,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   if (halo_eligible(a, hmode)) {
     const char* gm = getenv("RDMI_GEMM_GROUP");
     p.group_m = gm ? atoi(gm) : 8;
+    const char* cpp = getenv("RDMI_CONV_PIPE");
+    p.conv_pipe = !cpp || cpp[0] != '0';
     const char* cp = getenv("RDMI_CPERM");
     p.cperm = (!cp || cp[0] != '0') && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 &&
               (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0));
@@ -1600,12 +1649,16 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
 #undef RDMI_HALO
     } else {  // two workgroups per CU (RDMI_CONV_HALO=3: also for Cout % 256 == 0)
       dim3 g((a->Cout + 127) / 128, patches, 1);
-#define RDMI_OCC2(M)                                                                     \
-  do {                                                                                   \
-    if (gn)                                                                              \
-      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, true>), g, dim3(256), 0, st, p);      \
-    else                                                                                 \
-      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, false>), g, dim3(256), 0, st, p);     \
+#define RDMI_OCC2(M)                                                                               \
+  do {                                                                                             \
+    if (gn && p.conv_pipe)                                                                         \
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, true, true>), g, dim3(256), 0, st, p);          \
+    else if (gn)                                                                                   \
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, true, false>), g, dim3(256), 0, st, p);         \
+    else if (p.conv_pipe)                                                                          \
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, false, true>), g, dim3(256), 0, st, p);         \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<M, false, false>), g, dim3(256), 0, st, p);        \
   } while (0)
       if (a->upsample)
         RDMI_OCC2(2);

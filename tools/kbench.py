@@ -81,7 +81,7 @@ def bench_gnconv(iters):
             continue
 
         def unfused():
-            lib.rdmi_groupnorm_apply(x.data_ptr(), h.data_ptr(), B, H * W, ci, 32, mr.data_ptr(), g.data_ptr(),
+            lib.rdmi_groupnorm_apply(x.data_ptr(), h.data_ptr(), 0, B, H * W, ci, 32, mr.data_ptr(), g.data_ptr(),
                                      b.data_ptr(), 1, K._stream())
             K.conv2d(h, w, co, 3, upsample=up, out=out)
 
@@ -250,7 +250,7 @@ def bench_gn(iters):
         ms_s = timeit(lambda: K.groupnorm_stats(x, 32, 1e-5), iters)
         mr = K.groupnorm_stats(x, 32, 1e-5)
         from rollingdepth_amd._native import lib
-        ms_a = timeit(lambda: lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), B, HW, C, 32, mr.data_ptr(),
+        ms_a = timeit(lambda: lib.rdmi_groupnorm_apply(x.data_ptr(), out.data_ptr(), 0, B, HW, C, 32, mr.data_ptr(),
                                                        g.data_ptr(), b.data_ptr(), 1, K._stream()), iters)
         by = x.numel() * 2
         print(f"gn    {lab:32s} stats {ms_s * 1e3:8.1f} us {by / ms_s / 1e6:7.0f} GB/s | apply {ms_a * 1e3:8.1f} us "

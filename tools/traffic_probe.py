@@ -22,6 +22,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--what", default="conv")
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--batch", type=int, default=8)
+ap.add_argument("--res", type=int, default=768)
+ap.add_argument("--cin", type=int, default=128)
+ap.add_argument("--variant", default="full", choices=["full", "plain", "gn", "gnres"],
+                help="conv: full = GN input + residual + moments; plain = conv only; gn = GN input only; "
+                     "gnres = GN input + residual")
 a = ap.parse_args()
 torch.manual_seed(0)
 if a.what == "copy":
@@ -31,7 +36,7 @@ if a.what == "copy":
     fn = lambda: y.copy_(x)  # noqa: E731
     print(f"algorithmic: read {n * 2} B, write {n * 2} B per launch")
 elif a.what == "conv":
-    B, H, W, C = a.batch, 768, 768, 128
+    B, H, W, C = a.batch, a.res, a.res, a.cin
     x = torch.randn(B, H, W, C, device="cuda").half()
     res = torch.randn(B, H, W, C, device="cuda").half()
     gm = 1 + 0.1 * torch.randn(C, device="cuda")
@@ -41,8 +46,14 @@ elif a.what == "conv":
     mr = K.groupnorm_stats(x, 32, 1e-6)
     out = torch.empty(B, H, W, C, device="cuda", dtype=torch.float16)
 
+    ig = None if a.variant == "plain" else (mr, gm, bt, 32, True)
+    rr = res if a.variant in ("full", "gnres") else None
+    if ig is not None and not K.conv2d_in_gn_supported(x, w, C, 3, 32):
+        ig = None
+        print("GroupNorm input fusion not supported at this shape: unfused input")
+
     def fn():
-        K.conv2d(x, w, C, 3, bias=b, residual=res, out=out, gn=True, in_gn=(mr, gm, bt, 32, True))
+        K.conv2d(x, w, C, 3, bias=b, residual=rr, out=out, gn=a.variant == "full", in_gn=ig)
 
     act = B * H * W * C * 2
     print(f"algorithmic: read {2 * act + w.numel() * 2} B (input + residual + weights), write {act} B "
