@@ -26,7 +26,7 @@ Extra JSON fields: `roofline` for the dominant kernel family by summed time (ach
 FLOPs of every launch of that family in the timed steps ÷ their summed HIP-event durations, events
 recorded on the launch stream), with the fused attention reported beside it (`roofline.attention`);
 `roofline.traffic` = HBM bytes per launch of that family from the committed rocprofv3 PMC passes over
-one step of the same preset (profiles/bench_traffic.json, tools/pmc_bench.sh), beside the algorithmic
+one step of the same preset (bench_traffic.json, tools/pmc_bench.sh), beside the algorithmic
 bytes per launch (every operand read once, output written once) measured here;
 `cpu_baseline`: the CPU oracle (oracle/rd_oracle.py, fp32 PyTorch restatement of the reference
 pipeline, pinned to reference golden vectors) on this host — BASELINE configs[0] (3 frames 256²),
@@ -133,8 +133,9 @@ def _relaunch(n: int) -> int:
 
 def _pmc_traffic(preset: str, family: str):
     """HBM bytes per launch of `family` from the committed PMC passes over this preset's bench step
-    (tools/pmc_bench.sh → tools/bench_traffic.py → profiles/bench_traffic.json), or None."""
-    f = os.path.join(ROOT, "profiles", "bench_traffic.json")
+    (tools/pmc_bench.sh → tools/bench_traffic.py → bench_traffic.json; the per-kernel table is
+    profiles/r02_pmc_bench_fast.txt), or None."""
+    f = os.path.join(ROOT, "bench_traffic.json")
     try:
         ent = json.load(open(f))[preset]
         fam = ent["families"][family]

@@ -19,6 +19,8 @@
 #ifndef RDMI_H
 #define RDMI_H
 
+#include <stddef.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -31,6 +33,12 @@ extern "C" {
 /* storage dtype codes of the `dtype` arguments (f32 is the paper preset's arithmetic, run_video.py:444-449) */
 #define RDMI_F16 0
 #define RDMI_F32 1
+#define RDMI_U8 2 /* decoded video frames (rdmi_resize input) */
+
+/* rdmi_resize modes: torchvision InterpolationMode NEAREST / BILINEAR / BICUBIC */
+#define RDMI_RESIZE_NEAREST 0
+#define RDMI_RESIZE_BILINEAR 1
+#define RDMI_RESIZE_BICUBIC 2
 
 #define RDMI_EPI_NONE 0
 #define RDMI_EPI_GEGLU 1 /* out[:, n] = (h + b_h) * gelu_erf(g + b_g), weights row-interleaved */
@@ -283,6 +291,22 @@ int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, cons
                                void* stream);
 int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w, int f0, int nf, long HW,
                               const float* sum, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Frame ingest / resize.  Replaces load_video_frames' per-frame resize_max_res + normalisation
+ * (rollingdepth/video_io.py:38-67, 104-123: torchvision resize(antialias=True) of the decoded
+ * float frame, then (x / 255)·2 − 1) and __call__'s restore_res resizes
+ * (rollingdepth_pipeline.py:155-173).  x element (n, c, y, x) at x + n·sn + c·sc + y·sy + x·sx
+ * (elements) of dtype RDMI_U8 (decoded rgb24 frames, e.g. sn = H·W·3, sc = 1, sy = W·3, sx = 3) or
+ * RDMI_F32; y f32 [N, C, Ho, Wo] contiguous.  mode RDMI_RESIZE_*: the antialiased separable
+ * filter of F.interpolate(antialias=True) for BILINEAR / BICUBIC (width pass, then height pass;
+ * a dimension whose size does not change is not resampled), ATen nearest indexing for NEAREST.
+ * normalize != 0: y = (v / 255)·2 − 1.  Downscale factor ≤ 9 (bicubic ≤ 4.5).  workspace ≥
+ * rdmi_resize_workspace(...) bytes (f32 intermediate when both dimensions change).
+ */
+size_t rdmi_resize_workspace(int N, int C, int H, int W, int Ho, int Wo);
+int rdmi_resize(const void* x, int x_dtype, long sn, long sc, long sy, long sx, int N, int C, int H, int W, int Ho,
+                int Wo, int mode, int normalize, float* y, void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

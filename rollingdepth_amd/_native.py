@@ -90,6 +90,8 @@ _SIGS = {
     "rdmi_snippet_accumulate": (i32, [vp, i32, i32, i32, i32, i32, i32, i64, i32, i32, vp, vp]),
     "rdmi_snippet_finish": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
     "rdmi_colorize": (i32, [vp, i32, i64, vp, vp, i32, vp, vp, vp]),
+    "rdmi_resize_workspace": (C.c_size_t, [i32, i32, i32, i32, i32, i32]),
+    "rdmi_resize": (i32, [vp, i32, i64, i64, i64, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rdmi_minmax": (i32, [vp, i32, i64, vp, vp, vp]),
     "rdmi_renormalize_f32": (i32, [vp, i64, vp, vp]),
     "rdmi_aligner_workspace": (i64, [C.POINTER(AlignerArgs)]),
@@ -102,7 +104,8 @@ _SIGS = {
     "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), i32, i32, i32, i64, vp, vp, vp]),
 }
 
-RDMI_F16, RDMI_F32 = 0, 1
+RDMI_F16, RDMI_F32, RDMI_U8 = 0, 1, 2
+RDMI_RESIZE_NEAREST, RDMI_RESIZE_BILINEAR, RDMI_RESIZE_BICUBIC = 0, 1, 2
 
 EXPORTED = tuple(_SIGS)
 

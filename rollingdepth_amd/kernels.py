@@ -765,3 +765,45 @@ def aligner_merge_finish(sums: torch.Tensor, n: Sequence[int], strides: Sequence
     check(lib.rdmi_aligner_merge_finish(nd, nn, stv, w, f0, nf, HW, sums.data_ptr(), out.data_ptr(), _stream()),
           "rdmi_aligner_merge_finish")
     return out
+
+
+# ----------------------------------------------------------------------------- frame ingest / resize
+_RESIZE_MODES = {"NEAREST": _N.RDMI_RESIZE_NEAREST, "BILINEAR": _N.RDMI_RESIZE_BILINEAR,
+                 "BICUBIC": _N.RDMI_RESIZE_BICUBIC}
+
+
+def resize(x: torch.Tensor, size, mode: str = "BILINEAR", normalize: bool = False, channels_last: bool = False,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """rdmi_resize: torchvision resize(antialias=True) of a float / uint8 image batch → f32 [N, C, Ho, Wo].
+    x: [N, C, H, W] (any strides), or [N, H, W, C] with channels_last=True (decoded rgb24 frames).
+    normalize: (v / 255)·2 − 1 after the resize (video_io.py:123)."""
+    if not x.is_cuda:
+        raise ValueError(f"resize: expected a device tensor, got {x.device}")
+    if x.dtype == torch.uint8:
+        code = _N.RDMI_U8
+    elif x.dtype == F32:
+        code = _N.RDMI_F32
+    else:
+        raise TypeError(f"resize: uint8 or float32 input, got {x.dtype}")
+    if mode not in _RESIZE_MODES:
+        raise NotImplementedError(f"resize: interpolation {mode} (NEAREST, BILINEAR, BICUBIC)")
+    if x.dim() != 4:
+        raise ValueError(f"resize: 4-D input expected, got {tuple(x.shape)}")
+    if channels_last:
+        N, H, W, Cc = x.shape
+        sn, sy, sx, sc = x.stride()
+    else:
+        N, Cc, H, W = x.shape
+        sn, sc, sy, sx = x.stride()
+    Ho, Wo = int(size[0]), int(size[1])
+    if out is None:
+        out = torch.empty((N, Cc, Ho, Wo), dtype=F32, device=x.device)
+    if out.shape != (N, Cc, Ho, Wo) or out.dtype != F32 or not out.is_contiguous():
+        raise ValueError("resize: out must be a contiguous f32 [N, C, Ho, Wo] tensor")
+    ws = None
+    nb = lib.rdmi_resize_workspace(N, Cc, H, W, Ho, Wo)
+    if nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    check(lib.rdmi_resize(x.data_ptr(), code, sn, sc, sy, sx, N, Cc, H, W, Ho, Wo, _RESIZE_MODES[mode],
+                          int(normalize), out.data_ptr(), _p(ws), _stream()), "rdmi_resize")
+    return out

@@ -414,20 +414,38 @@ class RollingDepthPipeline:
                  refine_start_dilation: int = 6, generator: Union[torch.Generator, None] = None,
                  verbose: bool = False, max_vae_bs: int = 4, unload_snippet: bool = False,
                  restore_res: bool = False, input_fg_video_path=None, **kw) -> RollingDepthOutput:
-        """rollingdepth_pipeline.py:78-176.  Accepts a [N,3,H,W] tensor in [-1,1] in place of a
-        video path (video decoding needs PyAV, absent from this image)."""
+        """rollingdepth_pipeline.py:78-176.  `input_video_path` (or the fork's `input_fg_video_path`):
+        a video file (decoding needs PyAV, absent from this image), decoded uint8 rgb24 frames
+        [N, H, W, 3] (numpy / torch: resized to processing_res and normalised on the device,
+        video_io.load_video_frames), or an already-normalised float [N, 3, H, W] tensor in [-1, 1]
+        (used as is: processing_res and restore_res do not apply to it)."""
+        assert processing_res >= 0
+        if processing_res > 1024:
+            logging.warning(f"Procssing at high-resolution ({processing_res}) may lead to suboptimal accuracy.")
         src = input_fg_video_path if input_fg_video_path is not None else input_video_path
-        if isinstance(src, torch.Tensor):
+        original_res = None
+        if isinstance(src, torch.Tensor) and src.is_floating_point():
             frames = src
         else:
             from .video_io import load_video_frames
-            frames, _ = load_video_frames(src, start_frame, frame_count, processing_res, resample_method, verbose)
+            frames, original_res = load_video_frames(src, start_frame, frame_count, processing_res, resample_method,
+                                                     verbose, device=self.device)
         if restore_res:
-            raise NotImplementedError("restore_res needs torchvision resize (absent from this image)")
+            if original_res is None:
+                raise ValueError("restore_res needs the original resolution: pass the video or its decoded uint8 "
+                                 "frames, not a normalised tensor")
+            if max(original_res) > 2048:
+                logging.warning(f"Resizing back to large resolution ({list(original_res)}) may result in significant "
+                                "memory usage.")
         kw.pop("input_bg_video_path", None)  # fork CLI (run_video.py:563): IC-Light background, unused here
         out = self.forward(frames[None] if frames.dim() == 4 else frames, dilations, cap_dilation, snippet_lengths,
                            init_infer_steps, strides, coalign_kwargs, refine_step, refine_snippet_len,
                            refine_start_dilation, generator, verbose, max_vae_bs, unload_snippet, **kw)
+        if restore_res:  # rollingdepth_pipeline.py:155-173 (torchvision resize, antialias=True), on the device
+            for name in ("input_rgb", "depth_pred"):
+                t = getattr(out, name)
+                r = K.resize(t.to(self.device, torch.float32), original_res, resample_method.upper())
+                setattr(out, name, r.to(t.dtype).cpu())
         if input_fg_video_path is not None:
             rgb = out.depth_pred.float() * 0.5 + 0.5
             out.R_pred = out.G_pred = out.B_pred = rgb

@@ -1,11 +1,100 @@
-"""Video ingest (rollingdepth/video_io.py:71-137) — needs PyAV, which is not installed in this image.
-Kept as an explicit, loud boundary: the pipeline accepts frame tensors directly."""
+"""Video ingest and egress — rollingdepth/video_io.py.
+
+Decoding and encoding need PyAV (absent from this image): `load_video_frames` on a path and
+`write_video_from_numpy` raise ImportError saying so.  Everything after the decode runs on the
+device: given decoded rgb24 frames (what PyAV's `frame.to_ndarray(format="rgb24")` returns,
+uint8 [N, H, W, 3] — numpy or torch), `load_video_frames` uploads the uint8 frames (a quarter of
+the PCIe bytes of the reference's float frames) and resizes + normalises them in one librdmi pass
+(`rdmi_resize`: torchvision resize(antialias=True) then (x / 255)·2 − 1, video_io.py:104-123).
+`resize_max_res` is video_io.py:38-67 on the device."""
+from __future__ import annotations
+
+import os
+from typing import Tuple, Union
+
+import numpy as np
+import torch
+
+from . import kernels as K
 
 
-def load_video_frames(input_path, start_frame=0, frame_count=0, processing_res=0, resample_method="BILINEAR",
-                      verbose=False):
+def _target_size(h: int, w: int, max_edge_resolution: int) -> Tuple[int, int]:
+    """video_io.py:58-65 (Python float arithmetic, int() truncation)."""
+    downscale_factor = min(max_edge_resolution / w, max_edge_resolution / h)
+    return int(h * downscale_factor), int(w * downscale_factor)
+
+
+def resize_max_res(img: torch.Tensor, max_edge_resolution: int, resample_method: str = "BILINEAR") -> torch.Tensor:
+    """video_io.py:38-67: [B, C, H, W] (float32 or uint8, on the device) resized so that the longer edge
+    is max_edge_resolution, aspect ratio kept → f32 [B, C, h, w]."""
+    assert 4 == img.dim(), f"Invalid input shape {img.shape}"
+    h, w = _target_size(img.shape[-2], img.shape[-1], max_edge_resolution)
+    return K.resize(img, (h, w), str(resample_method).upper().split(".")[-1])
+
+
+def frames_from_rgb24(frames: Union[np.ndarray, torch.Tensor], processing_res: int = 0,
+                      resample_method: str = "BILINEAR", device="cuda") -> Tuple[torch.Tensor, Tuple[int, int]]:
+    """Decoded uint8 [N, H, W, 3] frames → (f32 [N, 3, h, w] in [-1, 1] on the device, (H, W)):
+    video_io.py:104-123 for every frame at once."""
+    if isinstance(frames, np.ndarray):
+        frames = torch.from_numpy(np.ascontiguousarray(frames))
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
+        raise ValueError(f"expected uint8 [N, H, W, 3] rgb24 frames, got {frames.dtype} {tuple(frames.shape)}")
+    if frames.shape[0] == 0:
+        raise RuntimeError("No frame is loaded")
+    n, h0, w0, _ = frames.shape
+    dev = frames.to(device, non_blocking=True)
+    h, w = _target_size(h0, w0, processing_res) if processing_res > 0 else (h0, w0)
+    out = K.resize(dev, (h, w), str(resample_method).upper().split(".")[-1], normalize=True, channels_last=True)
+    return out, (h0, w0)
+
+
+def load_video_frames(input_path, start_frame: int = 0, frame_count: int = 0, processing_res: int = 0,
+                      resample_method: str = "BILINEAR", verbose: bool = False, device="cuda"):
+    """video_io.py:71-137.  `input_path`: a video file (needs PyAV) or already-decoded uint8 rgb24
+    frames [N, H, W, 3] (numpy / torch).  Returns (f32 [N, 3, h, w] in [-1, 1] on `device`, (H, W))."""
+    assert start_frame >= 0
+    if isinstance(input_path, (np.ndarray, torch.Tensor)):
+        frames = input_path
+        end = start_frame + frame_count if frame_count > 0 else frames.shape[0]
+        frames = frames[start_frame:end]
+        if frames.shape[0] == 0:
+            raise RuntimeError("No frame is loaded from the given frames")
+        return frames_from_rgb24(frames, processing_res, resample_method, device)
+    if not isinstance(input_path, (str, os.PathLike)):
+        raise TypeError(f"load_video_frames: a path or uint8 [N, H, W, 3] frames, got {type(input_path)}")
+    try:
+        import av
+    except ImportError as e:
+        raise ImportError("video decoding needs PyAV, which is not installed in this image; decode the video "
+                          "elsewhere and pass the uint8 [N, H, W, 3] rgb24 frames instead") from e
+    container = av.open(input_path)  # pragma: no cover — PyAV absent here
+    try:
+        stream = container.streams.video[0]
+        stream.thread_type = "AUTO"
+        end_before = start_frame + frame_count if frame_count > 0 else np.inf
+        frame_ls = []
+        for i, frame in enumerate(container.decode(stream)):
+            if i >= end_before:
+                break
+            if i >= start_frame:
+                frame_ls.append(frame.to_ndarray(format="rgb24"))
+    finally:
+        container.close()
+    if not frame_ls:
+        raise RuntimeError(f"No frame is loaded from {input_path}")
+    return frames_from_rgb24(np.stack(frame_ls), processing_res, resample_method, device)
+
+
+def write_video_from_numpy(frames: np.ndarray, output_path, fps: int = 30, codec=None, crf: int = 23,
+                           preset: str = "medium", verbose: bool = False) -> None:
+    """video_io.py:140-208 — encoding needs PyAV (absent from this image)."""
+    if len(frames.shape) != 4 or frames.shape[-1] != 3:
+        raise ValueError(f"Expected shape [n, height, width, 3], got {frames.shape}")
+    if frames.dtype != np.uint8:
+        raise ValueError(f"Expected dtype uint8, got {frames.dtype}")
     try:
         import av  # noqa: F401
     except ImportError as e:
-        raise ImportError("video decoding needs PyAV (absent); pass a [N,3,H,W] tensor in [-1,1] instead") from e
-    raise NotImplementedError("video ingest is SURVEY.md §8f rank 3 (next rounds)")
+        raise ImportError("video encoding needs PyAV, which is not installed in this image") from e
+    raise NotImplementedError("video encoding (PyAV present but not wired in this build)")  # pragma: no cover

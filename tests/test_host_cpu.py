@@ -162,3 +162,22 @@ def test_empty_text_embedding_vs_transformers_and_reference(tmp_path):
         want = m(ids)[0]
     got = TE.empty_text_embedding(str(big))
     assert (got - want).abs().max().item() < 2e-5 * max(1.0, want.abs().max().item())
+
+
+def test_video_target_size_and_missing_pyav():
+    """video_io.py:58-65 target size (Python float arithmetic) and the loud PyAV boundary."""
+    from rollingdepth_amd import video_io as V
+
+    for (h, w, r) in [(1080, 1920, 768), (1080, 1920, 1024), (720, 1280, 768), (331, 197, 120), (100, 100, 768)]:
+        f = min(r / w, r / h)
+        assert V._target_size(h, w, r) == (int(h * f), int(w * f))
+    assert V._target_size(1080, 1920, 768) == (432, 768)
+    try:
+        import av  # noqa: F401
+    except ImportError:
+        with pytest.raises(ImportError, match="PyAV"):
+            V.load_video_frames("/nonexistent.mp4")
+        with pytest.raises(ImportError, match="PyAV"):
+            V.write_video_from_numpy(np.zeros((1, 4, 4, 3), np.uint8), "/tmp/x.mp4")
+    with pytest.raises(ValueError):
+        V.frames_from_rgb24(np.zeros((1, 4, 4, 4), np.uint8))

@@ -1,0 +1,120 @@
+"""Frame ingest / resize on the device (rdmi_resize) against the reference's arithmetic.
+
+The reference resizes decoded float frames with torchvision's `resize(..., antialias=True)`
+(rollingdepth/video_io.py:38-67) and normalises (x / 255)·2 − 1 (:123); restore_res resizes the
+outputs back the same way (rollingdepth_pipeline.py:155-173).  torchvision is absent here; its
+tensor resize is `torch.nn.functional.interpolate(mode, align_corners=False, antialias=True)`
+(BILINEAR / BICUBIC) and `interpolate(mode="nearest")` (NEAREST), which is what these tests run on
+the CPU as the oracle.  Tolerance: the GPU restates ATen's tap / weight arithmetic but not its
+vectorised summation order, so |Δ| ≤ 2e-6 on the normalised frames (≤ 3e-4 of one 8-bit level)
+and ≤ 1e-5 relative on resized f32 data; NEAREST is exact."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(n, h, w, seed=0):
+    g = np.random.default_rng(seed)
+    base = g.integers(0, 256, size=(n, h, w, 3), dtype=np.uint8)
+    # smooth content plus texture (both the low-pass and the alias-prone parts of the filter matter)
+    yy, xx = np.mgrid[0:h, 0:w]
+    smooth = (127.5 + 100 * np.sin(xx / 17.0 + yy / 23.0))[None, :, :, None]
+    return np.clip(0.5 * base + 0.5 * smooth, 0, 255).astype(np.uint8)
+
+
+def _ref_ingest(frames_u8, processing_res, mode):
+    """video_io.py:104-123 with torchvision's tensor resize spelled as F.interpolate."""
+    out = []
+    for fr in frames_u8:
+        f = torch.from_numpy(fr.copy()).float().permute(2, 0, 1)[None]
+        if processing_res > 0:
+            h0, w0 = f.shape[-2:]
+            s = min(processing_res / w0, processing_res / h0)
+            size = [int(h0 * s), int(w0 * s)]
+            if mode == "NEAREST":
+                f = F.interpolate(f, size=size, mode="nearest")
+            else:
+                f = F.interpolate(f, size=size, mode=mode.lower(), align_corners=False, antialias=True)
+        out.append((f / 255.0) * 2.0 - 1.0)
+    return torch.cat(out)
+
+
+@pytest.mark.parametrize("mode", ["BILINEAR", "BICUBIC", "NEAREST"])
+@pytest.mark.parametrize("shape,res", [((3, 270, 480), 256), ((2, 331, 197), 120), ((2, 64, 48), 100),
+                                       ((2, 90, 160), 0), ((1, 720, 1280), 768)])
+def test_ingest_matches_reference(mode, shape, res):
+    from rollingdepth_amd.video_io import load_video_frames
+
+    fr = _frames(*shape)
+    got, orig = load_video_frames(fr, processing_res=res, resample_method=mode)
+    want = _ref_ingest(fr, res, mode)
+    assert orig == shape[1:]
+    assert got.shape == want.shape, (got.shape, want.shape)
+    d = (got.cpu() - want).abs().max().item()
+    print(f"{mode} {shape} -> {tuple(want.shape[-2:])}: max |d| {d:.2e}")
+    assert d <= (0.0 if mode == "NEAREST" else 2e-6), d
+
+
+def test_ingest_frame_range_and_torch_input():
+    from rollingdepth_amd.video_io import load_video_frames
+
+    fr = _frames(6, 40, 60)
+    got, _ = load_video_frames(torch.from_numpy(fr), start_frame=2, frame_count=3, processing_res=30)
+    want = _ref_ingest(fr[2:5], 30, "BILINEAR")
+    assert got.shape == want.shape
+    assert (got.cpu() - want).abs().max().item() <= 2e-6
+
+
+@pytest.mark.parametrize("src,dst", [((45, 80), (135, 240)), ((64, 64), (64, 100)), ((96, 54), (71, 54)),
+                                     ((768, 432), (1080, 1920))])
+@pytest.mark.parametrize("mode", ["BILINEAR", "BICUBIC"])
+def test_restore_resize_f32(src, dst, mode):
+    """restore_res: f32 depth / rgb resized back to the video's resolution (up- and down-sampling,
+    one dimension only, both)."""
+    from rollingdepth_amd import kernels as K
+
+    torch.manual_seed(0)
+    x = torch.rand(2, 3, *src) * 2 - 1
+    want = F.interpolate(x, size=list(dst), mode=mode.lower(), align_corners=False, antialias=True)
+    got = K.resize(x.cuda(), dst, mode).cpu()
+    d = ((got - want).abs().max() / want.abs().max()).item()
+    print(f"{mode} {src}->{dst}: rel {d:.2e}")
+    assert d <= 1e-5, d
+
+
+def test_resize_rejects_bad_input():
+    from rollingdepth_amd import kernels as K
+
+    with pytest.raises(TypeError):
+        K.resize(torch.zeros(1, 3, 8, 8, device="cuda", dtype=torch.float16), (4, 4))
+    with pytest.raises(NotImplementedError):
+        K.resize(torch.zeros(1, 3, 8, 8, device="cuda"), (4, 4), "LANCZOS")
+    with pytest.raises(RuntimeError):  # downscale beyond the tap buffer is refused, not truncated
+        K.resize(torch.zeros(1, 1, 8, 800, device="cuda"), (8, 8))
+
+
+def test_call_with_decoded_frames_and_restore_res():
+    """__call__ on decoded uint8 frames: device ingest at processing_res, then restore_res back to
+    the video's resolution (rollingdepth_pipeline.py:112-173) — against the same pipeline fed the
+    reference-ingested tensor and resized back on the CPU."""
+    from rollingdepth_amd import config as C
+    from rollingdepth_amd.pipeline import RollingDepthPipeline
+
+    pipe = RollingDepthPipeline.from_synthetic(C.TINY_UNET, C.TINY_VAE, C.RD_SCHEDULER, device="cuda")
+    fr = _frames(9, 45, 60)
+    kw = dict(dilations=[1, 3], cap_dilation=True, snippet_lengths=[3], init_infer_steps=[1], strides=[1],
+              coalign_kwargs={"num_iterations": 50}, refine_step=0)
+    h, w = pipe.vae.latent_hw(24, 32)  # 45×60 at processing_res 32 → 24×32
+    noise = torch.randn(1, 4, h, w, generator=torch.Generator().manual_seed(3))
+    out = pipe(fr, processing_res=32, restore_res=True, init_noise=noise, **kw)
+    frames = _ref_ingest(fr, 32, "BILINEAR")
+    base = pipe(frames, init_noise=noise, **kw)
+    assert out.depth_pred.shape[-2:] == (45, 60) and out.input_rgb.shape[-2:] == (45, 60)
+    want = F.interpolate(base.depth_pred.float(), size=[45, 60], mode="bilinear", align_corners=False,
+                         antialias=True)
+    d = (out.depth_pred.float() - want).abs().max().item()
+    print(f"restore_res depth max |d| {d:.2e}")
+    assert d <= 2e-3, d  # f16 storage of the restored map

@@ -2,7 +2,7 @@
 bench step (tools/pmc_bench.sh: FETCH_SIZE and WRITE_SIZE need separate passes).
 
     python tools/bench_traffic.py --fetch gpurun_out/pmc_bench/fetch --write gpurun_out/pmc_bench/write \
-        --preset fast --source profiles/r02_pmc_bench_summary.txt --out profiles/bench_traffic.json
+        --preset fast --source profiles/r02_pmc_bench_fast.txt --out bench_traffic.json
 
 Reading rules (MI355X_MICROARCH.md § HBM): FETCH_SIZE (KB) reports ½ of the bytes of 16-B-per-lane
 streaming reads, `buffer_load … lds` included — doubled here, checked on a known-bytes copy
@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--preset", default="fast")
     ap.add_argument("--source", default="")
-    ap.add_argument("--out", default="profiles/bench_traffic.json")
+    ap.add_argument("--out", default="bench_traffic.json")
     ap.add_argument("--summary", default=None, help="also write a per-kernel table here")
     a = ap.parse_args()
     if a.summary:

@@ -2,7 +2,7 @@
 # HBM-traffic passes over one bench step (no warm-up, no validation, no CPU leg): FETCH_SIZE and
 # WRITE_SIZE in separate rocprofv3 runs (TCC slots: 3 + 2 > 4), each under its own kill timeout.
 #   PRESET=fast OUT=gpurun_out/pmc_bench bash tools/pmc_bench.sh
-# then tools/bench_traffic.py turns the two CSVs into profiles/bench_traffic.json.
+# then tools/bench_traffic.py turns the two CSVs into bench_traffic.json.
 set -e
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/pmc_bench}
