@@ -110,9 +110,9 @@ __device__ __forceinline__ int col_base(bool perm, int nw, int j, int fq) {
   return perm ? nw + 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : nw + j * 16 + fq * 4;
 }
 
-template <int RM, int RN, int WTN, class Rows>
-__device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
-                                           int fr, int fq, bool perm = false) {
+template <int RM, int RN, int WTN, bool SILU, class Rows>
+__device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
+                                             int fr, int fq, bool perm) {
   const long cb = (long)bz * p.sC;
   const long rbz = (long)bz * p.sR;
   // Fast path for whole f16 tiles (every row exists, every 4-column group inside N, one row-bias
@@ -159,7 +159,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
         for (int r = 0; r < 4; ++r) {
           float v = acc[i][j][r] * p.alpha + badd[j][r];
           if (p.R) v += (float)rr[i][j][r];
-          if (p.silu) v = silu_f(v);
+          if constexpr (SILU) v = silu_f(v);
           o[r] = (f16)v;
           const float f = (float)o[r];
           s += f;
@@ -225,7 +225,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] += (float)rr[r];
             }
-            if (p.silu) {
+            if constexpr (SILU) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = silu_f(v[r]);
             }
@@ -252,7 +252,7 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
               if (p.bias) x += p.bias[nn];
               if (rbrow) x += rbrow[nn];
               if (p.R) x += (float)p.R[rrow + nn];
-              if (p.silu) x = silu_f(x);
+              if constexpr (SILU) x = silu_f(x);
               if (p.c_f32)
                 ((float*)p.C)[crow + nn] = x;
               else
@@ -318,6 +318,18 @@ __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN],
       }
     }
   }
+}
+
+
+// The SiLU epilogue (TimestepEmbedding only) is a wave-uniform choice: dispatched here, outside the
+// per-output code, so that no other GEMM / conv computes (and discards) a SiLU per output.
+template <int RM, int RN, int WTN, class Rows>
+__device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
+                                           int fr, int fq, bool perm = false) {
+  if (p.silu)
+    store_tile_t<RM, RN, WTN, true>(p, acc, rows, nw, bz, fr, fq, perm);
+  else
+    store_tile_t<RM, RN, WTN, false>(p, acc, rows, nw, bz, fr, fq, perm);
 }
 
 using rdmi::tile_mn;
@@ -1284,6 +1296,329 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
 }
 
+// Halo conv with 32×32×16 MFMAs for 128-channel output tiles (the VAE's 768² / 384² convs with
+// Cout % 128 == 0 — in the pipeline the 128-channel decoder / encoder convs, GroupNorm input
+// included).  The two-workgroups-per-CU structure of conv_halo_occ2_kernel, re-cut for vector-issue
+// headroom: those convs are bound by the SIMD's vector-instruction issue, not by the matrix pipe
+// (SQ PMC, profiles/r02_pmc_conv_summary.txt: 4.2k–7.1k VALU per wave against 1 152 16×16×32 MFMAs,
+// each of which holds the vector issue for 8 of its 16 cycles).  Here
+//  * v_mfma_f32_32x32x16_f16 (8 of 32 cycles held): half the issue cost per FLOP of the MFMAs;
+//  * a 32×8 output patch (a 32-pixel fragment = one patch row), so that with the 16-B chunks of each
+//    halo pixel swizzled by its COLUMN, (col >> 1) & 7, every fragment read is conflict-free and its
+//    address is a per-lane register chosen by (tap dx, k-step) plus a compile-time immediate: the
+//    nine taps of a channel block are unrolled and the K loop carries no address arithmetic;
+//  * weight rows permuted within each 32-row block (perm32) so that a lane's 16 accumulator entries
+//    are 16 consecutive output channels (two 16-B stores / residual loads per fragment).
+// Workgroup = 4 waves: wm = wid >> 1 → patch rows 4wm..4wm+3, wn = wid & 1 → channels 64wn..+63;
+// wave tile 4 fragments (rows) × 2 fragments (32 channels) of 32×32.  LDS: the 10×34 halo of one
+// 64-channel block (43 KiB), a 2-slot weight ring (2 × 16 KiB), the GroupNorm table (2 KiB).
+// K order per output (channel block, tap, 16-k steps) as the other halo engines; the MFMA's own
+// 16-k reduction differs from the 32-k one of 16×16×32, so results match them to f32 rounding, not
+// bitwise.  Moments: per (fragment, 4-channel group) the lane's 4 channels, then the 32 pixels of
+// the fragment (rows of 16 lanes by DPP, the two rows by row_bcast:15).
+__device__ __forceinline__ int perm32(int m) { return ((m >> 2) & 1) * 16 + (m >> 3) * 4 + (m & 3); }
+
+template <int NKS>
+__device__ __forceinline__ void h32_sched() {
+  __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    if (ks + 1 < NKS) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+  }
+}
+
+template <bool GN>
+__global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
+  constexpr int BN = 128, BKP = 64;
+  constexpr int HR = 10, HC = 34, HPIX = HR * HC;  // halo of a 32×8 patch
+  constexpr int HPC = 43;                          // 8-pixel pieces (344 >= 340)
+  constexpr int HPW = 11;                          // piece slots per wave (44 >= 43)
+  constexpr int HALO = HPC * 8 * BKP;              // halves
+  constexpr int BSLOT = BN * BKP;                  // halves
+  constexpr int NB = 4;                            // weight pieces per wave per K-tile
+  constexpr int GNT = GN ? 256 : 0;
+  __shared__ __attribute__((aligned(16))) f16 lds[HALO + 2 * BSLOT + 4 * GNT];
+  float* const gnt = (float*)(lds + HALO + 2 * BSLOT);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int wids = __builtin_amdgcn_readfirstlane(wid);
+  const int nbx = gridDim.x;
+  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+  int mt_, nt_;
+  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  const int n0 = nt_ * BN;
+  const int pxn = p.Wo >> 5, pyn = p.Ho >> 3;
+  const int px = mt_ % pxn;
+  const int py = (mt_ / pxn) % pyn;
+  const int b = mt_ / (pxn * pyn);
+  const int y0 = py * 8, x0 = px * 32;
+  const __amdgpu_buffer_rsrc_t ra_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw_ =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.Wt, (short)0, (int)p.w_bytes, 0x00020000);
+
+  // DMA geometry: a 1-KiB piece = 8 pixel slots (or weight rows) × 8 physical 16-B chunks, lane L
+  // writing slot L >> 3, physical chunk L & 7, i.e. logical chunk (L & 7) ^ swizzle(slot)
+  const int lrow = lane >> 3, pc = lane & 7;
+  unsigned hoff[HPW];  // byte offset of this lane's 16 B of halo piece e in channel block 0, or OOB
+  // logical chunk of this lane in piece e (GroupNorm channels 8·lc .. +8 of the block)
+  auto hlc = [&](int e) {
+    const int hp = (wid + 4 * e) * 8 + lrow;
+    return pc ^ (((hp - (hp / HC) * HC) >> 1) & 7);
+  };
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) {
+    const int hp = (wid + 4 * e) * 8 + lrow;
+    const int hr = hp / HC, hc = hp - hr * HC;
+    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
+    const bool ok = hp < HPIX && (unsigned)yy < (unsigned)p.IH && (unsigned)xx < (unsigned)p.IW;
+    hoff[e] = ok ? (unsigned)((((b * p.IH + yy) * p.IW + xx) * p.Cin + hlc(e) * 8) * 2) : OOB;
+  }
+  unsigned boff[NB];
+#pragma unroll
+  for (int e = 0; e < NB; ++e) {
+    const int rt = (wid + 4 * e) * 8 + lrow;  // LDS row of the weight tile
+    const int n = n0 + (rt & ~31) + perm32(rt & 31);
+    const int lc = pc ^ ((rt >> 1) & 7);
+    boff[e] = n < p.N ? (unsigned)((n * (int)p.ldw + lc * 8) * 2) : OOB;
+  }
+  const int ncb = p.Cin >> 6;
+  auto hv = [&](int e) { return wids + 4 * e < HPC; };
+  auto issueHalo = [&](int cb) {
+#pragma unroll
+    for (int e = 0; e < HPW; ++e)
+      if (hv(e))
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (__attribute__((address_space(3))) void*)(lds + (wid + 4 * e) * 8 * BKP),
+                                                 16, hoff[e], cb * 128, 0, 0);
+  };
+  auto issueB = [&](int u) {
+    f16* lb = lds + HALO + (u & 1) * BSLOT;
+#pragma unroll
+    for (int e = 0; e < NB; ++e)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw_, (__attribute__((address_space(3))) void*)(lb + (wid + 4 * e) * 8 * BKP),
+                                               16, boff[e], u * 128, 0, 0);
+  };
+  unsigned inmask = 0;  // bit e: this lane's pixel of halo piece e lies inside the image
+#pragma unroll
+  for (int e = 0; e < HPW; ++e) inmask |= (hoff[e] != OOB ? 1u : 0u) << e;
+  auto xformHalo = [&](int cb) {
+    const int npc = (HPC - wids + 3) / 4;  // pieces of this wave
+#pragma unroll 1
+    for (int e = 0; e < npc; ++e) {
+      {
+        f16* lh = lds + (wid + 4 * e) * 8 * BKP + lane * 8;
+        const float* ts = gnt + cb * 64 + hlc(e) * 8;
+        const f32x4 s0 = *(const f32x4*)ts, s1 = *(const f32x4*)(ts + 4);
+        const f32x4 h0 = *(const f32x4*)(ts + GNT), h1 = *(const f32x4*)(ts + GNT + 4);
+        const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+        const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const f16x8 v = *(const f16x8*)lh;
+        const bool in = (inmask >> e) & 1;
+        f16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float f = fmaf((float)v[i], sc[i], sh[i]);
+          if (p.gsilu) f = silu_f(f);
+          o[i] = in ? (f16)f : (f16)0.f;
+        }
+        *(f16x8*)lh = o;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+
+  // fragment addresses (bytes from lds): pixel j = lane & 31 of a fragment row, k-step ks reads
+  // logical chunk 2ks + hh of halo slot (row 4wm + pb + dy, column j + dx), physical chunk
+  // logical ^ (((j + dx) >> 1) & 7); weights: row 64wn + 32chb + j, physical chunk
+  // logical ^ ((row >> 1) & 7) (32chb does not change (row >> 1) & 7)
+  const int j = lane & 31, hh = lane >> 5;
+  const unsigned lds0 = (unsigned)(uintptr_t)LDS_PTR(f16, lds);
+  unsigned poff[3][4], woff[4];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      poff[dx][ks] = lds0 + (unsigned)(((4 * wm * HC + j + dx) * BKP + (((2 * ks + hh) ^ (((j + dx) >> 1) & 7)) << 3)) * 2);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int row = 64 * wn + j;
+    woff[ks] = lds0 + (unsigned)((HALO + row * BKP + (((2 * ks + hh) ^ ((row >> 1) & 7)) << 3)) * 2);
+  }
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][c][r] = 0.f;
+
+  // prologue: halo(0), B(0) [, GroupNorm scale/shift of image b]
+  issueHalo(0);
+  issueB(0);
+  if constexpr (GN) {
+    const int c = tid;
+    float mean = 0.f, rstd = 0.f, gm = 0.f, bt = 0.f;
+    if (c < p.Cin) {
+      const int g = c / (p.Cin / p.gG);
+      mean = p.gmr[2 * (b * p.gG + g)];
+      rstd = p.gmr[2 * (b * p.gG + g) + 1];
+      gm = p.ggam[c];
+      bt = p.gbet[c];
+    }
+    const float sc = rstd * gm;
+    gnt[c] = sc;
+    gnt[GNT + c] = bt - mean * sc;
+  }
+  wait_vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr (GN) {
+    xformHalo(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("" ::: "memory");
+
+  // one K-tile: tap TAP of channel block cb, weights in slot PAR
+  auto ktile = [&](auto TAPc, auto PARc, int cb) {
+    constexpr int TAP = decltype(TAPc)::value, PAR = decltype(PARc)::value;
+    constexpr int dy = TAP / 3, dx = TAP % 3;
+    const int u = cb * 9 + TAP;
+    if (u > 0) {
+      if (TAP == 0) {  // refill the halo with channel block cb
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is past its reads of halo(cb-1)
+        asm volatile("" ::: "memory");
+        issueHalo(cb);
+        wait_vmcnt<0>();  // B(u) and this wave's halo pieces
+        if constexpr (GN) xformHalo(cb);
+      } else {
+        wait_vmcnt<0>();  // B(u), issued one K-tile ago
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of B(u-1) done (slot reuse)
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (u + 1 < 9 * ncb) issueB(u + 1);
+    f16x8 af[2][2], bf[2][4];
+    auto rd = [&](int ks, int buf) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        af[buf][c] = *(const f16x8*)LDS_PTR(f16, (uintptr_t)(woff[ks] + (PAR * BSLOT + c * 32 * BKP) * 2));
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb)
+        bf[buf][pb] = *(const f16x8*)LDS_PTR(f16, (uintptr_t)(poff[dx][ks] + ((pb + dy) * HC * BKP) * 2));
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks + 1 < 4) rd(ks + 1, (ks + 1) & 1);
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc[pb][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[ks & 1][c], bf[ks & 1][pb], acc[pb][c], 0, 0, 0);
+    }
+    h32_sched<4>();
+  };
+  auto block = [&](auto PAR0, int cb) {  // the nine taps of channel block cb, slot parity alternating
+    constexpr int P0 = decltype(PAR0)::value;
+    ktile(std::integral_constant<int, 0>{}, std::integral_constant<int, P0>{}, cb);
+    ktile(std::integral_constant<int, 1>{}, std::integral_constant<int, P0 ^ 1>{}, cb);
+    ktile(std::integral_constant<int, 2>{}, std::integral_constant<int, P0>{}, cb);
+    ktile(std::integral_constant<int, 3>{}, std::integral_constant<int, P0 ^ 1>{}, cb);
+    ktile(std::integral_constant<int, 4>{}, std::integral_constant<int, P0>{}, cb);
+    ktile(std::integral_constant<int, 5>{}, std::integral_constant<int, P0 ^ 1>{}, cb);
+    ktile(std::integral_constant<int, 6>{}, std::integral_constant<int, P0>{}, cb);
+    ktile(std::integral_constant<int, 7>{}, std::integral_constant<int, P0 ^ 1>{}, cb);
+    ktile(std::integral_constant<int, 8>{}, std::integral_constant<int, P0>{}, cb);
+  };
+  for (int cb = 0; cb < ncb; cb += 2) {  // ncb even (h32_ok): K-tile u = 9cb + tap uses slot u & 1
+    block(std::integral_constant<int, 0>{}, cb);
+    block(std::integral_constant<int, 1>{}, cb + 1);
+  }
+  wait_vmcnt<0>();  // drain trailing DMAs before the workgroup can retire
+
+  // ---- epilogue: fragment (pb, c) = pixels (y0 + 4wm + pb, x0 + j), channels nb .. nb + 15.
+  // The optional parts are wave-uniform: one instantiation per (residual, SiLU) so that neither is
+  // if-converted into every output.
+  const long rbg = p.rowbias ? (long)b * p.rb_ld : 0;  // conv row bias: one group per image
+  auto epilogue = [&](auto RESc, auto SILUc) {
+    constexpr bool RES = decltype(RESc)::value, SILU = decltype(SILUc)::value;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int nb = n0 + 64 * wn + 32 * c + 16 * hh;
+      f32x4 badd[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        badd[q] = p.bias ? *(const f32x4*)(p.bias + nb + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (p.rowbias) badd[q] += *(const f32x4*)(p.rowbias + rbg + nb + 4 * q);
+      }
+      f16x8 rr[4][2];
+      if constexpr (RES) {
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          const long m = (long)(b * p.Ho + y0 + 4 * wm + pb) * p.Wo + x0 + j;
+          const f16* rrow = p.R + m * p.ldr + nb;
+          rr[pb][0] = *(const f16x8*)rrow;
+          rr[pb][1] = *(const f16x8*)(rrow + 8);
+        }
+      }
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const long m = (long)(b * p.Ho + y0 + 4 * wm + pb) * p.Wo + x0 + j;
+        f16x8 ov[2];
+        float gs[4], gq[4];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float v = acc[pb][c][i] * p.alpha + badd[i >> 2][i & 3];
+          if constexpr (RES) v += (float)rr[pb][i >> 3][i & 7];
+          if constexpr (SILU) v = silu_f(v);
+          const f16 o = (f16)v;
+          ov[i >> 3][i & 7] = o;
+          const float f = (float)o;
+          if ((i & 3) == 0) {
+            gs[i >> 2] = f;
+            gq[i >> 2] = f * f;
+          } else {
+            gs[i >> 2] += f;
+            gq[i >> 2] = fmaf(f, f, gq[i >> 2]);
+          }
+        }
+        f16* crow = (f16*)p.C + m * p.ldc + nb;
+        *(f16x8*)crow = ov[0];
+        *(f16x8*)(crow + 8) = ov[1];
+        if (p.gnp) {  // slot (4-channel group, 32 pixels of this fragment row)
+          const long slot = ((long)(b * p.Ho + y0 + 4 * wm + pb) * p.Wo + x0) >> 5;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float s = row16_sum(gs[g]), q = row16_sum(gq[g]);
+            s += dpp_f<0x142>(s);  // row_bcast:15 — rows 1 and 3 add the sums of rows 0 and 2
+            q += dpp_f<0x142>(q);
+            if ((lane & 31) == 16) {
+              float* d = p.gnp + (long)((nb + 4 * g) >> 2) * p.gn_ld + slot * 2;
+              d[0] = s;
+              d[1] = q;
+            }
+          }
+        }
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (p.R) {
+    if (p.silu) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  } else {
+    if (p.silu) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+  }
+}
+
 // Two-workgroups-per-CU dense GEMM (the UNet's single-batch Linears).  A 256×256
 // ping-pong tile over K = 320 runs only 5 K-tiles between a DMA prologue and a 128-KiB epilogue
 // that one workgroup per CU cannot overlap, and such GEMMs move as many bytes (A in, C out) as
@@ -1525,6 +1860,20 @@ bool in_gn_ok(const rdmi_conv_args* a) {
   return a->in_groups > 0 && a->Cin <= cmax && a->Cin % a->in_groups == 0;
 }
 
+// conv_halo32_kernel: no upsample, Cout % 128 == 0, Cin % 128 == 0 (channel blocks in pairs), 32×8
+// patches, 16-B epilogue accesses, input GroupNorm table ≤ 256 channels.  Opt-in (RDMI_CONV_H32=1):
+// measured against conv_halo_occ2_kernel on the 768² 128-channel conv (tools/conv_ab.py,
+// tools/pmc_conv_ab.sh, profiles/r02_pmc_conv_ab.txt) it cuts VALU per wave 3.4k → 1.5k and lifts
+// MFMA-busy 0.60 → 0.63, but the chip is power-limited there (1.43–1.71 GHz under these loads) and
+// the clock drops by as much: −2…+4 % plain, −4…−6 % with the GroupNorm input + residual.
+bool h32_ok(const rdmi_conv_args* a, const GemmP& p, bool gn) {
+  const char* e = getenv("RDMI_CONV_H32");
+  if (!e || e[0] != '1') return false;
+  return !a->upsample && a->Cout % 128 == 0 && a->Cin % 128 == 0 && a->Ho % 8 == 0 && a->Wo % 32 == 0 && p.vec && !p.c_f32 &&
+         ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 && (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0)) &&
+         (!p.bias || ((uintptr_t)p.bias & 15) == 0) && (!gn || a->Cin <= 256);
+}
+
 }  // namespace
 
 extern "C" int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* a) {
@@ -1647,6 +1996,12 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
       else
         RDMI_HALO(1, 1, 2);
 #undef RDMI_HALO
+    } else if (h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches
+      dim3 g(a->Cout / 128, (unsigned)((a->Ho / 8) * (a->Wo / 32) * a->B), 1);
+      if (gn)
+        hipLaunchKernelGGL((conv_halo32_kernel<true>), g, dim3(256), 0, st, p);
+      else
+        hipLaunchKernelGGL((conv_halo32_kernel<false>), g, dim3(256), 0, st, p);
     } else {  // two workgroups per CU (RDMI_CONV_HALO=3: also for Cout % 256 == 0)
       dim3 g((a->Cout + 127) / 128, patches, 1);
 #define RDMI_OCC2(M)                                                                               \

@@ -98,8 +98,10 @@ def test_gemm_geglu(engine):
     (2, 32, 48, 128, 256, 3, 1, 1, False), (1, 16, 16, 64, 512, 3, 1, 1, False), (1, 8, 16, 192, 256, 3, 1, 1, True),
     (3, 16, 32, 320, 256, 3, 1, 1, False), (2, 32, 16, 128, 128, 3, 1, 1, False), (1, 16, 8, 256, 128, 3, 1, 1, True),
     (1, 16, 32, 128, 384, 3, 1, 1, False), (2, 16, 16, 640, 640, 3, 1, 1, False), (1, 8, 8, 192, 384, 3, 1, 1, True),
-    (2, 16, 32, 320, 320, 3, 1, 1, False), (1, 16, 16, 960, 320, 3, 1, 1, False), (1, 16, 16, 64, 64, 3, 1, 1, False)])
-def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine):
+    (2, 16, 32, 320, 320, 3, 1, 1, False), (1, 16, 16, 960, 320, 3, 1, 1, False), (1, 16, 16, 64, 64, 3, 1, 1, False),
+    # 32×32×16 halo conv (conv_halo32_kernel: Cout, Cin % 128 == 0, Ho % 8, Wo % 32)
+    (2, 16, 64, 128, 128, 3, 1, 1, False), (1, 24, 32, 256, 128, 3, 1, 1, False), (1, 16, 96, 128, 384, 3, 1, 1, False)])
+def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine, h32):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(3)
     x = torch.randn(B, Cin, H, W, device=DEV, generator=g).half()
@@ -157,8 +159,9 @@ def test_groupnorm(C, G, HW, silu, eps):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,up", [(2, 16, 16, 64, 128, False), (3, 12, 12, 128, 256, True),
                                                 (1, 24, 20, 256, 512, False), (2, 16, 32, 128, 256, False),
-                                                (2, 8, 8, 64, 256, True), (2, 16, 32, 128, 128, False)])
-def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine):
+                                                (2, 8, 8, 64, 256, True), (2, 16, 32, 128, 128, False),
+                                                (1, 16, 64, 256, 128, False)])
+def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine, h32):
     """Conv epilogue-emitted GroupNorm moments (rdmi.h gn_part) vs the standalone stats pass and an
     fp32 reference; the moments of each image are bitwise independent of the batch they ran in."""
     K_ = _k()
@@ -205,8 +208,9 @@ def test_groupnorm_moments_from_gemm(engine):
     (2, 32, 48, 128, 256, False, True, 32), (1, 16, 16, 512, 512, False, True, 32), (2, 8, 16, 256, 256, True, True, 32),
     (2, 32, 16, 128, 128, False, True, 32), (1, 16, 8, 256, 128, True, False, 32), (3, 16, 32, 320, 256, False, True, 32),
     (1, 16, 16, 1024, 256, False, True, 16), (2, 16, 16, 64, 128, False, True, 8),
-    (2, 16, 16, 128, 384, False, True, 32), (1, 16, 16, 256, 640, True, True, 32), (2, 16, 16, 192, 320, False, True, 32)])
-def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G, engine):
+    (2, 16, 16, 128, 384, False, True, 32), (1, 16, 16, 256, 640, True, True, 32), (2, 16, 16, 192, 320, False, True, 32),
+    (2, 16, 64, 128, 128, False, True, 32), (1, 16, 32, 256, 128, False, True, 32), (2, 16, 32, 128, 128, False, False, 32)])
+def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G, engine, h32):
     """GroupNorm(+SiLU) applied inside the halo conv's input path (rdmi_conv_args.in_*) against the
     unfused groupnorm → conv2d pair on the same data: the same normalised f16 values feed the same
     MFMA order, so the outputs agree bitwise; plus an fp32 torch reference.  Images get distinct
@@ -236,6 +240,48 @@ def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G, engine):
     # the helper picks the fused path and matches as well
     y2 = K_.gn_conv2d(x, gm, bt, G, 1e-6, silu, wp, Cout, 3, upsample=up, bias=b)
     assert torch.equal(y2, y_ref)
+
+
+@pytest.fixture(params=["0", "1"])
+def h32(request, monkeypatch):
+    """conv_halo32_kernel opt-in (RDMI_CONV_H32) for the conv tests that cover its shapes."""
+    monkeypatch.setenv("RDMI_CONV_H32", request.param)
+    return request.param
+
+
+def test_conv2d_h32_epilogue(monkeypatch):
+    """The 32×32×16 halo conv's epilogue (bias, per-image row bias, residual, input GroupNorm+SiLU,
+    GroupNorm moments of the output) against an fp32 torch reference and against the
+    two-workgroups-per-CU 16×16×32 engine (RDMI_CONV_H32=0) — f32 rounding apart (the MFMA's k
+    reduction differs), and bitwise batch-invariant."""
+    K_ = _k()
+    monkeypatch.setenv("RDMI_CONV_H32", "1")
+    g = torch.Generator(device=DEV).manual_seed(31)
+    B, H, W, Cin, Cout = 3, 16, 64, 256, 128
+    x = (torch.randn(B, H, W, Cin, device=DEV, generator=g) * 1.3 + 0.2).half()
+    w = torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9)
+    wp = K_.pack_conv(w, DEV)
+    b = torch.randn(Cout, device=DEV, generator=g)
+    rb = torch.randn(B, Cout, device=DEV, generator=g)
+    res = torch.randn(B, H, W, Cout, device=DEV, generator=g).half()
+    gm = 1 + 0.2 * torch.randn(Cin, device=DEV, generator=g)
+    bt = 0.2 * torch.randn(Cin, device=DEV, generator=g)
+    mr = K_.groupnorm_stats(x, 32, 1e-6)
+
+    def run(xx, i0, i1):
+        return K_.conv2d(xx, wp, Cout, 3, bias=b, rowbias=rb[i0:i1], residual=res[i0:i1], gn=True,
+                         in_gn=(mr[i0 * 64:i1 * 64], gm, bt, 32, True))
+
+    y = run(x, 0, B)
+    hf = F.silu(F.group_norm(x.float().permute(0, 3, 1, 2), 32, gm, bt, 1e-6))
+    ref = F.conv2d(hf, w.to(DEV), b, padding=1) + rb[:, :, None, None] + res.float().permute(0, 3, 1, 2)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
+    mr_y = K_.groupnorm_stats(y, 32, 1e-6)
+    assert torch.allclose(mr_y, K_.groupnorm_stats(y.clone(), 32, 1e-6), rtol=1e-5, atol=1e-6)
+    assert torch.equal(run(x[1:2], 1, 2), y[1:2])
+    monkeypatch.setenv("RDMI_CONV_H32", "0")
+    y_occ2 = run(x, 0, B)
+    assert _rel(y, y_occ2) < 2e-3
 
 
 def test_conv2d_fused_input_groupnorm_unsupported():
