@@ -69,7 +69,11 @@ def bench_head(iters):
 def bench_gnconv(iters):
     """GroupNorm+SiLU → conv: apply pass + conv vs the norm fused into the halo conv's input."""
     from rollingdepth_amd._native import lib
-    for lab, B, H, W, ci, co, up in conv_cases()[5:]:
+    cases = conv_cases()[5:] + [("unet L0 320->320 96^2 x48", 48, 96, 96, 320, 320, False),
+                                ("unet L1 640->640 48^2 x48", 48, 48, 48, 640, 640, False),
+                                ("unet L0 640->320 96^2 x48", 48, 96, 96, 640, 320, False),
+                                ("unet L1 320->640 48^2 x48", 48, 48, 48, 320, 640, False)]
+    for lab, B, H, W, ci, co, up in cases:
         x = torch.randn(B, H, W, ci, device="cuda").half()
         w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
         g, b = torch.ones(ci, device="cuda"), torch.zeros(ci, device="cuda")
