@@ -1752,12 +1752,13 @@ void launch_pp(const GemmP& p, int batch, hipStream_t s) {
 template <int MODE>
 void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
   if (MODE == 0) {
-    // measured policy (tools/kbench.py gemm, profiles/r01_gemm_occ2_ab.log): the two-workgroups-
-    // per-CU engine wins on the UNet's single-batch Linears without a 256×256 ping-pong tile
-    // (N % 256 != 0: +4…18 %) or with a long K (N = 1280, K = 5120: +19 %), and loses on the
-    // GEGLU projections, the batched VAE attention GEMMs and N % 256 == 0 with short K (−9…18 %)
+    // measured policy (tools/gemm_policy_ab.py at the pipeline's shapes, profiles/r02_gemm_policy_ab.log,
+    // after the epilogue fix): the two-workgroups-per-CU engine wins on the UNet's single-batch
+    // Linears whose N has no 128-wide ping-pong tile (L0: N = 320 / 960, +17…24 %); with one
+    // (N % 128 == 0: L1 N = 640 / 1920, L2 N = 1280 at K = 5120) the 512×128 / 256×256 ping-pong
+    // tiles win by 3…17 %; it loses on the GEGLU projections and the batched VAE attention GEMMs
     const int oc = occ2_mode();
-    const bool pick = !p.geglu && batch == 1 && !p.c_f32 && p.N <= 1920 && (p.N % 256 != 0 || p.K >= 2048);
+    const bool pick = !p.geglu && batch == 1 && !p.c_f32 && p.N <= 1920 && p.N % 128 != 0;
     if (oc == 2 || (oc == 1 && pick)) {
       dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
       hipLaunchKernelGGL(gemm_occ2_kernel, g, dim3(256), 0, s, p);
@@ -1788,7 +1789,9 @@ void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
       if (c < best) best = c, pick = 1;
     }
     if (p.N % 128 == 0) {
-      const double c = tile_cost(mt512 * (p.N / 128) * batch, 512, 128, 1.0);  // measured ≈ classic per area
+      // measured 1.06–1.11× the classic engine per area at the L1 Linears and the VAE 1×1 conv
+      // (profiles/r02_gemm_policy_ab.log, after the epilogue fix)
+      const double c = tile_cost(mt512 * (p.N / 128) * batch, 512, 128, 1.1);
       if (c < best) best = c, pick = 3;
     }
     switch (pick) {
