@@ -292,6 +292,16 @@ int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, cons
 int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w, int f0, int nf, long HW,
                               const float* sum, float* out, void* stream);
 
+/* Single-head flash attention for head dim 512 (f16): the VAE mid-block attention
+ * (unet_2d_blocks.py:680-697 through AttnProcessor2_0's 4-D path, attention_processor.py:2172-2276 —
+ * one head, d = C = 512) as one pass over K / Vᵀ instead of f32 scores → softmax → PV.
+ * q [B][Sq][512] (row stride q_ld), k [B][Sk][512] (k_ld), vt = Vᵀ [B][512][Skp] (row stride vt_ld ≥
+ * Skp, Skp = Sk rounded up to 32, columns Sk..Skp-1 zero), o [B][Sq][512] (o_ld); batch strides in
+ * elements; o = softmax(q kᵀ · scale) v with f32 accumulation and f32 softmax statistics. */
+int rdmi_attention_d512(const void* q, const void* k, const void* vt, void* o, int B, int Sq, int Sk, int Skp,
+                        long q_ld, long k_ld, long vt_ld, long o_ld, long q_bs, long k_bs, long vt_bs, long o_bs,
+                        float scale, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Frame ingest / resize.  Replaces load_video_frames' per-frame resize_max_res + normalisation
  * (rollingdepth/video_io.py:38-67, 104-123: torchvision resize(antialias=True) of the decoded

@@ -526,6 +526,8 @@ def attention_1head(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: fl
     probabilities."""
     B, Sq, D = q.shape
     Sk = k.shape[1]
+    if D == 512 and q.dtype == F16 and os.environ.get("RDMI_VAE_FLASH", "1") != "0":
+        return attention_d512(q, k, v, scale)
     s = gemm(q, k, D, out_f32=True)
     Sp = (Sk + 7) // 8 * 8
     p = softmax_rows(s, scale, out=torch.empty((B, Sq, Sp), dtype=q.dtype, device=q.device))
@@ -533,6 +535,25 @@ def attention_1head(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: fl
     vt = torch.zeros((B, D, Sp), dtype=q.dtype, device=q.device) if Sp != Sk else None
     vt = transpose(v, out=vt)
     return gemm(p, vt, Sp)
+
+
+def attention_d512(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: float) -> torch.Tensor:
+    """rdmi_attention_d512: single-head flash attention at head dim 512 (the VAE mid-block).
+    q [B, Sq, 512], k / v [B, Sk, 512] (row strides any, 16-B aligned) → [B, Sq, 512] f16.  V is
+    transposed once into a zero-padded [B, 512, ceil32(Sk)] buffer (the kernel's PV operand)."""
+    B, Sq, D = q.shape
+    Sk = k.shape[1]
+    if D != 512 or q.dtype != F16 or k.dtype != F16 or v.dtype != F16:
+        raise ValueError("attention_d512: f16 q / k / v with head dim 512")
+    Skp = (Sk + 31) // 32 * 32
+    vt = torch.zeros((B, D, Skp), dtype=F16, device=q.device) if Skp != Sk else None
+    vt = transpose(v, out=vt)
+    o = torch.empty((B, Sq, D), dtype=F16, device=q.device)
+    with _Timed("attention_d512", 4.0 * B * Sq * Sk * D, f"attn512 B={B} S={Sq}", 2 * B * D * (2 * Sq + 2 * Sk)):
+        check(lib.rdmi_attention_d512(q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), B, Sq, Sk, Skp,
+                                      q.stride(1), k.stride(1), vt.stride(1), o.stride(1), q.stride(0), k.stride(0),
+                                      vt.stride(0), o.stride(0), float(scale), _stream()), "rdmi_attention_d512")
+    return o
 
 
 def transpose(src: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

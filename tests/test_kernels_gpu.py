@@ -490,6 +490,54 @@ def test_vae_style_attention_via_gemm(S):
         assert torch.equal(K_.gemm(p, K_.transpose(v), S), o)
 
 
+@pytest.mark.parametrize("B,Sq,Sk", [(2, 576, 576), (1, 2304, 2304), (2, 100, 100), (1, 300, 77), (1, 9216, 9216)])
+def test_attention_d512(B, Sq, Sk):
+    """Flash attention at head dim 512 (the VAE mid-block, rdmi_attention_d512) against an f64
+    softmax reference on the same f16 inputs (rows sampled at the full 768² size), and against the
+    GEMM → softmax → GEMM path; keys that are not a multiple of 32 are masked."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(41)
+    D = 512
+    qkv = torch.randn(B, max(Sq, Sk), 3 * D, device=DEV, generator=g).half()
+    q, k, v = qkv[:, :Sq, :D], qkv[:, :Sk, D:2 * D], qkv[:, :Sk, 2 * D:]
+    sc = 1.0 / math.sqrt(D)
+    o = K_.attention_d512(q, k, v, sc)
+    rows = torch.arange(Sq, device=DEV) if Sq <= 2304 else torch.randint(0, Sq, (256,), device=DEV, generator=g)
+    s = torch.einsum("bqd,bkd->bqk", q[:, rows].double(), k.double()) * sc
+    ref = torch.softmax(s, -1) @ v.double()
+    err = (o[:, rows].double() - ref).abs().max().item()
+    print(f"d512 B={B} Sq={Sq} Sk={Sk}: max |d| {err:.2e} (|ref| {ref.abs().max().item():.2f})")
+    assert err < 4e-3
+    if Sq <= 2304:
+        import os
+        os.environ["RDMI_VAE_FLASH"] = "0"
+        try:
+            o_gemm = K_.attention_1head(q.contiguous(), k.contiguous(), v.contiguous(), sc)
+        finally:
+            os.environ.pop("RDMI_VAE_FLASH")
+        assert (o.float() - o_gemm.float()).abs().max().item() < 4e-3
+
+
+def test_attention_d512_rescale():
+    """Scores that grow along the keys (the running max re-set several times, O / l rescaled) and
+    large scores (P at the edge of the f16 range before a rescale)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(42)
+    B, S, D = 1, 640, 512
+    q = (torch.randn(B, S, D, device=DEV, generator=g) * 1.5).half()
+    growth = torch.linspace(0.2, 4.0, S, device=DEV)[None, :, None]
+    k = (torch.randn(B, S, D, device=DEV, generator=g) * growth).half()
+    v = torch.randn(B, S, D, device=DEV, generator=g).half()
+    sc = 1.0 / math.sqrt(D)
+    o = K_.attention_d512(q, k, v, sc)
+    s = torch.einsum("bqd,bkd->bqk", q.double(), k.double()) * sc
+    ref = torch.softmax(s, -1) @ v.double()
+    err = (o.double() - ref).abs().max().item()
+    print(f"d512 rescale: max |d| {err:.2e}, score range {s.min().item():.1f}..{s.max().item():.1f}")
+    assert torch.isfinite(o).all()
+    assert err < 8e-3
+
+
 def test_layout_and_elementwise():
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(11)

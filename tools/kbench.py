@@ -241,6 +241,21 @@ def bench_attn(iters):
         print(f"attn  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
 
+def bench_attn512(iters):
+    """VAE mid-block attention (1 head, d = 512): flash kernel vs GEMM → softmax → GEMM."""
+    for B, S in [(16, 9216), (75, 9216), (16, 2304)]:
+        qkv = torch.randn(B, S, 1536, device="cuda").half()
+        q, k, v = qkv[..., :512], qkv[..., 512:1024], qkv[..., 1024:]
+        sc = 1.0 / math.sqrt(512)
+        fl = 4.0 * B * S * S * 512
+        ms_f = timeit(lambda: K.attention_d512(q, k, v, sc), iters)
+        os.environ["RDMI_VAE_FLASH"] = "0"
+        ms_g = timeit(lambda: K.attention_1head(q, k, v, sc), iters)
+        os.environ.pop("RDMI_VAE_FLASH")
+        print(f"attn512 B={B} S={S}: flash {ms_f * 1e3:9.1f} us {fl / ms_f / 1e9:7.1f} TF/s | gemm-softmax-gemm "
+              f"{ms_g * 1e3:9.1f} us {fl / ms_g / 1e9:7.1f} TF/s", flush=True)
+
+
 def bench_gn(iters):
     for lab, B, HW, C in [("unet 320 96^2 x24", 24, 9216, 320), ("vae 128 768^2 x8", 8, 589824, 128),
                           ("vae 256 384^2 x8", 8, 147456, 256), ("vae 512 96^2 x15", 15, 9216, 512),
@@ -268,4 +283,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
+        {"attn512": bench_attn512, "conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
