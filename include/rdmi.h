@@ -297,10 +297,13 @@ int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w,
  * one head, d = C = 512) as one pass over K / Vᵀ instead of f32 scores → softmax → PV.
  * q [B][Sq][512] (row stride q_ld), k [B][Sk][512] (k_ld), vt = Vᵀ [B][512][Skp] (row stride vt_ld ≥
  * Skp, Skp = Sk rounded up to 32, columns Sk..Skp-1 zero), o [B][Sq][512] (o_ld); batch strides in
- * elements; o = softmax(q kᵀ · scale) v with f32 accumulation and f32 softmax statistics. */
+ * elements; o = softmax(q kᵀ · scale) v with f32 accumulation and f32 softmax statistics.
+ * flags: int workspace of B·ceil(Sq / 128) entries (no initialisation needed) enabling the
+ * 32-query-per-wave pass with a fixed running max and a fix-up pass over the blocks it flags; NULL
+ * runs the 16-query kernel (running max with rescale) alone.  Same result either way. */
 int rdmi_attention_d512(const void* q, const void* k, const void* vt, void* o, int B, int Sq, int Sk, int Skp,
                         long q_ld, long k_ld, long vt_ld, long o_ld, long q_bs, long k_bs, long vt_bs, long o_bs,
-                        float scale, void* stream);
+                        float scale, int* flags, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Frame ingest / resize.  Replaces load_video_frames' per-frame resize_max_res + normalisation

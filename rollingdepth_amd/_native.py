@@ -91,7 +91,7 @@ _SIGS = {
     "rdmi_snippet_finish": (i32, [vp, i32, i32, i32, i32, i64, i32, i32, vp, i32, vp]),
     "rdmi_colorize": (i32, [vp, i32, i64, vp, vp, i32, vp, vp, vp]),
     "rdmi_resize_workspace": (C.c_size_t, [i32, i32, i32, i32, i32, i32]),
-    "rdmi_attention_d512": (i32, [vp, vp, vp, vp, i32, i32, i32, i32] + [i64] * 8 + [C.c_float, vp]),
+    "rdmi_attention_d512": (i32, [vp, vp, vp, vp, i32, i32, i32, i32] + [i64] * 8 + [C.c_float, vp, vp]),
     "rdmi_resize": (i32, [vp, i32, i64, i64, i64, i64, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rdmi_minmax": (i32, [vp, i32, i64, vp, vp, vp]),
     "rdmi_renormalize_f32": (i32, [vp, i64, vp, vp]),

@@ -549,10 +549,15 @@ def attention_d512(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, scale: flo
     vt = torch.zeros((B, D, Skp), dtype=F16, device=q.device) if Skp != Sk else None
     vt = transpose(v, out=vt)
     o = torch.empty((B, Sq, D), dtype=F16, device=q.device)
+    flags = None
+    if os.environ.get("RDMI_D512_W4", "0") == "1":  # opt-in: measured slower (693 vs 816 TF/s)
+        flags = torch.empty((B * ((Sq + 127) // 128),), dtype=torch.int32, device=q.device)
     with _Timed("attention_d512", 4.0 * B * Sq * Sk * D, f"attn512 B={B} S={Sq}", 2 * B * D * (2 * Sq + 2 * Sk)):
         check(lib.rdmi_attention_d512(q.data_ptr(), k.data_ptr(), vt.data_ptr(), o.data_ptr(), B, Sq, Sk, Skp,
                                       q.stride(1), k.stride(1), vt.stride(1), o.stride(1), q.stride(0), k.stride(0),
-                                      vt.stride(0), o.stride(0), float(scale), _stream()), "rdmi_attention_d512")
+                                      vt.stride(0), o.stride(0), float(scale),
+                                      flags.data_ptr() if flags is not None else None, _stream()),
+              "rdmi_attention_d512")
     return o
 
 

@@ -490,8 +490,15 @@ def test_vae_style_attention_via_gemm(S):
         assert torch.equal(K_.gemm(p, K_.transpose(v), S), o)
 
 
+@pytest.fixture(params=["w4", "w8"])
+def d512_kernel(request, monkeypatch):
+    """w4: the 32-query pass (fixed running max) + fix-up; w8: the 16-query kernel alone."""
+    monkeypatch.setenv("RDMI_D512_W4", "1" if request.param == "w4" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("B,Sq,Sk", [(2, 576, 576), (1, 2304, 2304), (2, 100, 100), (1, 300, 77), (1, 9216, 9216)])
-def test_attention_d512(B, Sq, Sk):
+def test_attention_d512(B, Sq, Sk, d512_kernel):
     """Flash attention at head dim 512 (the VAE mid-block, rdmi_attention_d512) against an f64
     softmax reference on the same f16 inputs (rows sampled at the full 768² size), and against the
     GEMM → softmax → GEMM path; keys that are not a multiple of 32 are masked."""
@@ -518,13 +525,19 @@ def test_attention_d512(B, Sq, Sk):
         assert (o.float() - o_gemm.float()).abs().max().item() < 4e-3
 
 
-def test_attention_d512_rescale():
-    """Scores that grow along the keys (the running max re-set several times, O / l rescaled) and
-    large scores (P at the edge of the f16 range before a rescale)."""
+@pytest.mark.parametrize("mixed", [False, True])
+def test_attention_d512_rescale(d512_kernel, mixed):
+    """Scores that grow along the keys (the running max re-set several times, O / l rescaled; for
+    the 32-query pass: its blocks flagged and recomputed by the fix-up) and large scores (P at the
+    edge of the f16 range before a rescale).  mixed: only the odd 128-query blocks grow past the
+    f16 range, so flagged and unflagged blocks share one launch."""
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(42)
     B, S, D = 1, 640, 512
-    q = (torch.randn(B, S, D, device=DEV, generator=g) * 1.5).half()
+    qs = torch.full((S, 1), 1.5, device=DEV)
+    if mixed:
+        qs[(torch.arange(S, device=DEV) // 128) % 2 == 0] = 0.05
+    q = (torch.randn(B, S, D, device=DEV, generator=g) * qs).half()
     growth = torch.linspace(0.2, 4.0, S, device=DEV)[None, :, None]
     k = (torch.randn(B, S, D, device=DEV, generator=g) * growth).half()
     v = torch.randn(B, S, D, device=DEV, generator=g).half()
