@@ -109,6 +109,14 @@ typedef struct rdmi_conv_args {
   /* RDMI_F16 or RDMI_F32 (x, w, y, residual).  f32 weights are always [Cout][kh][kw][Cin] (tap-major,
    * Kp % 32 == 0), Cin % 4 == 0, no input GroupNorm and no GroupNorm moments. */
   int dtype;
+  /* Optional, upsample = 1 only: the same conv's weights for the phase-decomposed form — the ×2
+   * nearest upsample + 3×3 conv computed as four 2×2 convs on the source grid, one per output
+   * phase (a, c) = (y & 1, x & 1), the 3×3 taps that read the same source pixel summed
+   * (rows {0 | 1,2} for a = 0, {0,1 | 2} for a = 1; columns likewise): 4/9 of the MFMA work.
+   * Layout [4 phases (2a + c)][Cout][Cin/64][2][2][64] f16 (row stride 4·Cin).  Used where the
+   * 256-channel halo engine runs the conv (f16, Cout % 256 == 0, Cin % 64 == 0, Ho % 32 == 0,
+   * Wo % 32 == 0, no input GroupNorm); elsewhere `w` is used.  NULL: off. */
+  const void* w_up2;
 } rdmi_conv_args;
 int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
 /* 1 if rdmi_conv2d fuses an input GroupNorm for this shape (in_groups set; pointers not read) */

@@ -44,6 +44,7 @@ class ConvArgs(C.Structure):
         ("gn_part", vp), ("gn_ld", i64),
         ("in_mean_rstd", vp), ("in_gamma", vp), ("in_beta", vp), ("in_groups", i32), ("in_silu", i32),
         ("dtype", i32),
+        ("w_up2", vp),
     ]
 
 

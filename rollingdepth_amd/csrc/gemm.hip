@@ -95,6 +95,19 @@ struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; H
   __device__ bool full(int) const { return true; }
   __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }  // conv: rpg = Ho·Wo
 };
+// Output phase (a, c) of a ×2-upsampled conv computed on the source grid (conv_halo_kernel MODE 3):
+// phase-grid patch rows y0 + rw + i, columns x0 + fr → output pixel (2y + a, 2x + c) of the
+// Ho × Wo output.  Moment slots: image b's range [b·HoWo/32, (b+1)·HoWo/32) split into the four
+// phases' sub-ranges of (Ho/2)(Wo/2)/32 slots, each laid out as PatchRows' on the phase grid.
+struct PhaseRows {
+  int b, Ho, Wo, y0, x0, rw, fr, a, c;
+  __device__ int row(int i) const { return (b * Ho + 2 * (y0 + rw + i) + a) * Wo + 2 * (x0 + fr) + c; }
+  __device__ long slot(int i) const {
+    return (long)(b * 4 + 2 * a + c) * ((Ho >> 1) * (Wo >> 1) >> 5) + ((y0 + rw + i - 1) >> 1) * (Wo >> 5) + (x0 >> 4);
+  }
+  __device__ bool full(int) const { return true; }
+  __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }
+};
 
 // 16-B epilogue accesses for the halo convs (p.cperm).  The weight rows are DMA'd into LDS in a
 // permuted order (perm64 within each wave's 64-channel slab) so that MFMA fragments 2q and 2q+1
@@ -801,8 +814,16 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 // ends with lgkmcnt(0); the last write (tap 8 phase 0) is ≥ 2 barriers before the first read of
 // block cb+1 by the group running one barrier ahead.  Halo pixels outside the image stay zero (the conv's zero padding is
 // applied after the norm).  Halo(0) is normalised in the prologue.
+// MODE 3: nearest ×2 upsample + 3×3 conv as four 2×2 convs on the source grid, one per output
+// phase (a, c) = (y & 1, x & 1) (the 3×3 taps that land on the same source pixel summed into one
+// weight: rows {0 | 1, 2} for a = 0, {0, 1 | 2} for a = 1, likewise columns; zero padding maps to
+// zero padding), 4/9 of MODE 2's MFMA work.  A tile is 16×16 pixels of one phase; its 17×17 source
+// halo (origin (y0 − 1 + a, x0 − 1 + c)) sits in the 18×18 halo buffer; weights p.Wt + phase·N·ldw
+// in the cmaj order with 4 taps (dy, dx) ∈ {0, 1}²; halo(cb+1) pieces 0-2 issued in tap 1, 3-5 in
+// tap 2, all landed by tap 3's wait.
 template <int MODE, int NPH, int WN, bool GN>
 __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
+  constexpr int NT = MODE == 3 ? 4 : 9;    // taps per channel block
   constexpr int WM = 8 / WN;
   constexpr int BN = WN * 64, BKP = 64, RM = 16 / WM, RN = 4;
   constexpr int NRG = NPH == 4 ? 2 : NPH;  // row groups of a wave (one per phase group)
@@ -818,6 +839,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   constexpr int GNT = GN ? 1024 : 0;       // GroupNorm scale/shift table: sc[1024], sh[1024] floats
   static_assert(RPG == 4 && (NPH != 1 || WN == 2) && (WN != 2 || NPH == 1) && (!GN || NPH != 4),
                 "unsupported halo variant");
+  static_assert(MODE != 3 || (NPH == 2 && WN == 4 && !GN), "phase-decomposed upsample: NPH 2, WN 4, no GN");
   __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + NBS * BSLOT + 4 * GNT];
   float* const gnt = (float*)(lds + 2 * HALO + NBS * BSLOT);
 
@@ -831,10 +853,13 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   int mt_, nt_;
   tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
   const int n0 = nt_ * BN;
-  const int pxn = p.Wo >> 4, pyn = p.Ho >> 4;
+  // MODE 3: m-tile = (image, phase, 16×16 tile of the Ho/2 × Wo/2 phase grid)
+  const int pxn = p.Wo >> (MODE == 3 ? 5 : 4), pyn = p.Ho >> (MODE == 3 ? 5 : 4);
   const int px = mt_ % pxn;
   const int py = (mt_ / pxn) % pyn;
-  const int b = mt_ / (pxn * pyn);
+  const int phs = MODE == 3 ? (mt_ / (pxn * pyn)) & 3 : 0;
+  const int b = mt_ / (pxn * pyn * (MODE == 3 ? 4 : 1));
+  const int pa = phs >> 1, pc = phs & 1;
   const int y0 = py * 16, x0 = px * 16;
   const __amdgpu_buffer_rsrc_t ra_ =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
@@ -850,7 +875,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   for (int e = 0; e < HPW; ++e) {
     const int hp = (wid + 8 * e) * 8 + lrow;
     const int hr = hp / HWD, hc = hp - hr * HWD;
-    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
+    const int yy = y0 - 1 + pa + hr, xx = x0 - 1 + pc + hc;
     const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
     hoff[e] = ok ? ((b * p.IH + sy) * p.IW + sx) * p.Cin : -1;
@@ -860,7 +885,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   for (int e = 0; e < NB; ++e) {
     const int rt = (wid + 8 * e) * 8 + lrow;  // LDS row of the tile
     const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
-    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+    brow[e] = n < p.N ? (phs * p.N + n) * (int)p.ldw : -1;
   }
   const int ncb = p.Cin >> 6;
   const int wids = __builtin_amdgcn_readfirstlane(wid);
@@ -887,7 +912,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = ncb * 9;
+  const int nk = ncb * NT;
   const int fr = lane & 15, fq = lane >> 4;
   const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
   const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
@@ -959,12 +984,12 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   const int wms = __builtin_amdgcn_readfirstlane(wm);
   f16x8 af[NKH][4] = {}, bf[2][RN] = {};
   for (int u = 0; u < nk; ++u) {
-    const int cb = u / 9;  // wave-uniform
-    const int tap = u - cb * 9;
-    const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+    const int cb = u / NT;  // wave-uniform
+    const int tap = u - cb * NT;
+    const int dy = MODE == 3 ? tap >> 1 : (tap * 11) >> 5, dx = MODE == 3 ? tap & 1 : tap - 3 * dy;
     const f16* lh = lds + (cb & 1) * HALO;
     const f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT + (wn * 64) * BKP;
-    const bool halo_now = tap >= 1 && tap <= HPW && hv(tap - 1);
+    const bool halo_now = MODE != 3 && tap >= 1 && tap <= HPW && hv(tap - 1);
     // halo pixel of fragment row r = RM·wm + 4·rg + i, lane fr: hp = (r + dy)·18 + dx + fr, whose
     // swizzle term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or rg (RM·18, 72 ≡ 0 mod 8)
     const int xb = fr + dx + 2 * dy;
@@ -1003,6 +1028,26 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
           issueB(u + 2, 2, 4);
         }
         if (ph == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else if (NPH == 2 && MODE == 3) {
+        if (ph == 0) {
+          if (tap == 1) {
+#pragma unroll
+            for (int e = 0; e < 3; ++e) issueHalo(cb + 1, e);
+          } else if (tap == 2) {
+#pragma unroll
+            for (int e = 3; e < HPW; ++e)
+              if (hv(e)) issueHalo(cb + 1, e);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B(u) read for the last time
+        } else {
+          if (tap == 1)
+            wait_vmcnt<3>();  // B(u+1) landed (halo pieces 0-2 in flight)
+          else if (tap == 2)
+            wait_vmcnt<2>();  // B(u+1) and pieces 0-2 landed (3-4, and 5 on wave 0, in flight)
+          else
+            wait_vmcnt<0>();  // B(u+1) (and on tap 3 all of halo(cb+1)) landed
+          issueB(u + 2, 0, NB);
+        }
       } else if (NPH == 2) {
         if (ph == 0) {
           if (halo_now) issueHalo(cb + 1, tap - 1);
@@ -1053,7 +1098,11 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   if (grp == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
 
-  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+  if constexpr (MODE == 3)
+    store_tile<RM, RN, 64>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr, fq,
+                           p.cperm);
+  else
+    store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
 }
 
 // Issue-order pins for conv_halo_occ2_kernel's pipelined K-tile (sched_group_barrier needs
@@ -1971,7 +2020,12 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
     const bool gn = p.gmr != nullptr;
-    if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256))) {
+    if (a->upsample && a->w_up2 && !gn && a->Cout % 256 == 0 && a->Ho % 32 == 0 && a->Wo % 32 == 0 && hmode != 3 &&
+        al16(a->w_up2)) {  // phase-decomposed ×2 upsample conv (4 taps per phase)
+      p.Wt = (const f16*)a->w_up2; p.ldw = 4L * a->Cin; p.K = p.Kvalid = 4 * a->Cin;
+      p.w_bytes = (unsigned)(4L * a->Cout * p.ldw * 2);
+      hipLaunchKernelGGL((conv_halo_kernel<3, 2, 4, false>), dim3(a->Cout / 256, patches, 1), dim3(512), 0, st, p);
+    } else if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256))) {
       dim3 g(a->Cout / 256, patches, 1);
       const bool ph2 = hmode != 1 || gn;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
 #define RDMI_HALO(M, P, WN)                                                     \

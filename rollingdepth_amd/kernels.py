@@ -134,6 +134,30 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16)
     return out.to(device)
 
 
+def pack_conv_up2(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> Optional[torch.Tensor]:
+    """3×3 weights [Cout, Cin, 3, 3] of a conv behind a nearest ×2 upsample → the four output
+    phases' 2×2 weights (rdmi.h rdmi_conv_args.w_up2): [4 (2a + c), Cout, 4·Cin_pad] f16 in the
+    order [Cin_pad/64][dy][dx][64].  Phase a reads source rows (i − 1 + a, i + a): 3×3 rows {0}, {1, 2}
+    for a = 0 and {0, 1}, {2} for a = 1 land on them (columns likewise), so their weights are
+    summed — in f32 from the checkpoint's values, rounded to f16 once.  None when Cin_pad % 64."""
+    co, ci, kh, kw = w.shape
+    cp = cin_pad or pad_channels(ci)
+    if (kh, kw) != (3, 3) or cp % 64:
+        return None
+    sets = (((0,), (1, 2)), ((0, 1), (2,)))
+    wf = w.float()
+    out = torch.zeros((4, co, cp // 64, 2, 2, 64), dtype=F32)
+    for a in range(2):
+        for c in range(2):
+            for dy in range(2):
+                for dx in range(2):
+                    t = sum(wf[:, :, ky, kx] for ky in sets[a][dy] for kx in sets[c][dx])  # [Cout, Cin]
+                    tp = torch.zeros((co, cp), dtype=F32)
+                    tp[:, :ci] = t
+                    out[2 * a + c, :, :, dy, dx, :] = tp.reshape(co, cp // 64, 64)
+    return out.reshape(4, co, 4 * cp).to(F16).to(device)
+
+
 # ----------------------------------------------------------------------------- GEMM / conv
 def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] = None,
          bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
@@ -221,7 +245,8 @@ def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, 
     return g
 
 
-def _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn):
+def _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn,
+               w_up2=None):
     B, H, W, Cin = x.shape
     pt = pad if pad_tl is None else pad_tl
     a = _N.ConvArgs()
@@ -231,6 +256,7 @@ def _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, row
     a.B, a.H, a.W, a.Cin, a.Cout, a.kh, a.kw = B, H, W, Cin, cout, k, k
     a.stride, a.pad_top, a.pad_left, a.upsample, a.Ho, a.Wo = stride, pt, pt, int(upsample), Ho, Wo
     a.Kp = w.shape[1]
+    a.w_up2 = _p(w_up2) if upsample else None
     a.y_ld = out.stride(-2) if out is not None else 0
     a.res_ld = residual.stride(-2) if residual is not None else 0
     a.alpha = alpha
@@ -253,9 +279,11 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
            pad_tl: Optional[int] = None, upsample: bool = False, bias: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, rowbias: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, alpha: float = 1.0, out_hw=None, gn: bool = False,
-           in_gn=None, _gn_slot=None) -> torch.Tensor:
+           in_gn=None, _gn_slot=None, w_up2: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NHWC f16 conv.  x [B, H, W, Cin_pad]; w packed by pack_conv.  `pad` is symmetric; pad_tl
     overrides the top/left padding with bottom/right implied by out_hw (VAE Downsample2D).
+    w_up2 (upsample only): pack_conv_up2's phase weights, which the library runs where its
+    phase-decomposed form applies (RDMI_UP2=0 turns it off).
     gn=True: also emit the output's GroupNorm moments (as gemm).
     in_gn=(mean_rstd, gamma, beta, groups, silu): GroupNorm(+SiLU) of x applied as it is read
     (rdmi.h rdmi_conv_args.in_*; only where conv2d_in_gn_supported)."""
@@ -289,26 +317,44 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
             conv2d(x[s0:s1], w, cout, k, stride, pad, pad_tl, upsample, bias,
                    None if residual is None else residual[s0:s1],
                    rb if rb is not None or rowbias is None else rowbias[s0:s1],
-                   out[s0:s1], alpha, out_hw, in_gn=ig, _gn_slot=slot)
+                   out[s0:s1], alpha, out_hw, in_gn=ig, _gn_slot=slot, w_up2=w_up2)
         _gn_attach(out, part)
         return out
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
-    a = _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn)
+    if w_up2 is not None and (f32 or os.environ.get("RDMI_UP2", "1") == "0"):
+        w_up2 = None
+    if w_up2 is not None and (w_up2.dtype != F16 or tuple(w_up2.shape) != (4, cout, 4 * Cin) or
+                              not w_up2.is_contiguous()):
+        raise ValueError(f"conv2d: w_up2 must be pack_conv_up2's [4, {cout}, {4 * Cin}] f16")
+    a = _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn,
+                   w_up2)
     a.dtype = _N.RDMI_F32 if f32 else _N.RDMI_F16
     if part is not None:
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
         a.gn_part, a.gn_ld = _gn_slot
     es = x.element_size()
-    nb = es * (x.numel() + cout * k * k * Cin + (2 if residual is not None else 1) * B * Ho * Wo * cout)
-    with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * B * Ho * Wo * cout * k * k * Cin,
+    # executed MFMA work: 4 taps per output pixel where the phase-decomposed upsample runs (whose
+    # weights are the 4 phases × 4 taps)
+    taps = 4 if (w_up2 is not None and _up2_runs(a)) else k * k
+    nb = es * (x.numel() + cout * (16 if taps == 4 else k * k) * Cin +
+               (2 if residual is not None else 1) * B * Ho * Wo * cout)
+    with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * B * Ho * Wo * cout * taps * Cin,
                 f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}",
                 nb):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")
     if _gn_slot is None:
         _gn_attach(out, part)
     return out
+
+
+def _up2_runs(a) -> bool:
+    """Mirror of rdmi_conv2d's choice of the phase-decomposed upsample form (gemm.hip)."""
+    hm = int(os.environ.get("RDMI_CONV_HALO", "2"))
+    return (a.upsample == 1 and bool(a.w_up2) and not a.in_mean_rstd and a.Cout % 256 == 0 and a.Ho % 32 == 0 and
+            a.Wo % 32 == 0 and hm not in (0, 3) and a.kh == 3 and a.kw == 3 and a.Cin % 64 == 0 and a.stride == 1 and
+            a.pad_top == 1 and a.pad_left == 1 and a.Ho == 2 * a.H and a.Wo == 2 * a.W)
 
 
 # conv2d splits its batch when the input reaches 2 GiB (the kernels' 32-bit buffer byte offsets)

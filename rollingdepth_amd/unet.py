@@ -51,11 +51,13 @@ class _Lin:
 
 
 class _Conv:
-    def __init__(self, sd, key, dev, stride=1, pad=1, dtype=F16):
+    def __init__(self, sd, key, dev, stride=1, pad=1, dtype=F16, up2=False):
+        """up2: the conv of an Upsample2D — also pack the phase-decomposed weights (K.pack_conv_up2)."""
         w = sd[key + ".weight"]
         self.cout, self.cin, self.k, _ = w.shape
         self.cin_pad = K.pad_channels(self.cin)
         self.w = K.pack_conv(w, dev, self.cin_pad, dtype)
+        self.w_up2 = K.pack_conv_up2(w, dev, self.cin_pad) if up2 and dtype == F16 else None
         self.b = sd[key + ".bias"].to(dev, F32) if key + ".bias" in sd else None
         self.stride, self.pad = stride, pad
 
@@ -63,7 +65,7 @@ class _Conv:
         """gn=True when a GroupNorm consumes the output (its moments come from this epilogue)."""
         return K.conv2d(x, self.w, self.cout, self.k, stride=self.stride, pad=self.pad, pad_tl=pad_tl,
                         upsample=upsample, bias=self.b, residual=residual, rowbias=rowbias, out=out, out_hw=out_hw,
-                        gn=gn)
+                        gn=gn, w_up2=self.w_up2 if upsample else None)
 
     def normed(self, x, norm, groups, eps, silu=True, residual=None, rowbias=None, gn=False):
         """self(silu?(GroupNorm(x))), the norm fused into the conv's input path where supported."""
@@ -240,7 +242,7 @@ class UNet:
                 if bt == "CrossAttnUpBlock2D":
                     blk["attn"].append(Transformer(sd, f"up_blocks.{i}.attentions.{j}", dev, rheads[i], g, dtype))
             if i < len(ch) - 1:
-                blk["us"] = _Conv(sd, f"up_blocks.{i}.upsamplers.0.conv", dev, dtype=dtype)
+                blk["us"] = _Conv(sd, f"up_blocks.{i}.upsamplers.0.conv", dev, dtype=dtype, up2=True)
             self.up.append(blk)
         self.norm_out = _Norm(sd, "conv_norm_out", dev)
         self.conv_out = _Conv(sd, "conv_out", dev, dtype=dtype)

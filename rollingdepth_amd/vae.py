@@ -29,6 +29,7 @@ class _FoldedConv(_Conv):
         self.cout, self.cin, self.k, _ = w.shape
         self.cin_pad = K.pad_channels(self.cin)
         self.w = K.pack_conv(w, dev, self.cin_pad, dtype)
+        self.w_up2 = None
         self.b = b.to(dev, F32)
         self.stride, self.pad = stride, pad
 
@@ -102,7 +103,8 @@ class VAE:
         self.d_up = []
         for i in range(len(ch)):
             res = [R(f"decoder.up_blocks.{i}.resnets.{j}") for j in range(L + 1)]
-            us = _Conv(sd, f"decoder.up_blocks.{i}.upsamplers.0.conv", dev, dtype=dtype) if i < len(ch) - 1 else None
+            us = _Conv(sd, f"decoder.up_blocks.{i}.upsamplers.0.conv", dev, dtype=dtype, up2=True) \
+                if i < len(ch) - 1 else None
             self.d_up.append((res, us))
         self.d_norm = _Norm(sd, "decoder.conv_norm_out", dev)
         wd, bd = sd["decoder.conv_out.weight"], sd["decoder.conv_out.bias"]

@@ -69,6 +69,34 @@ def test_pack_conv_channel_block_major():
     assert torch.equal(K.pack_conv(w1, "cpu").float(), w1[:, :, 0, 0].half().float())
 
 
+def test_pack_conv_up2_phase_identity():
+    """pack_conv_up2: conv3×3(nearest×2(x)) == the four 2×2 phase convs on the source grid
+    (rdmi.h rdmi_conv_args.w_up2) — the identity the GPU's phase-decomposed upsample relies on,
+    checked in f64 on the packed weights' f16 values (and the phase tensor's layout)."""
+    from rollingdepth_amd import kernels as K
+
+    torch.manual_seed(0)
+    B, Cin, Cout, H, W = 2, 128, 8, 5, 7
+    x = torch.randn(B, Cin, H, W, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3)
+    wu = K.pack_conv_up2(w, "cpu")
+    assert wu.shape == (4, Cout, 4 * Cin) and wu.dtype == torch.float16
+    wph = wu.double().view(4, Cout, Cin // 64, 2, 2, 64).permute(0, 1, 2, 5, 3, 4).reshape(4, Cout, Cin, 2, 2)
+    ref = torch.nn.functional.conv2d(torch.nn.functional.interpolate(x, scale_factor=2.0, mode="nearest"),
+                                     w.double(), padding=1)
+    xp = torch.nn.functional.pad(x, (1, 1, 1, 1))
+    got = torch.empty_like(ref)
+    for a in range(2):
+        for c in range(2):
+            got[:, :, a::2, c::2] = torch.nn.functional.conv2d(xp[:, :, a:a + H + 1, c:c + W + 1], wph[2 * a + c])
+    # f16 rounding of the summed weights only
+    assert (got - ref).abs().max().item() < 2e-3 * ref.abs().max().item()
+    exact = wu.double().view(4, Cout, Cin // 64, 2, 2, 64)
+    assert torch.equal(exact[0, :, :, 1, 1], (w[:, :, 1:, 1:].sum((2, 3))).half().double().view(Cout, 2, 64))
+    assert torch.equal(exact[3, :, :, 0, 0], (w[:, :, :2, :2].sum((2, 3))).half().double().view(Cout, 2, 64))
+    assert K.pack_conv_up2(torch.randn(4, 32, 3, 3), "cpu") is None  # Cin_pad % 64 != 0
+
+
 def test_geglu_permutation_roundtrip():
     from rollingdepth_amd import kernels as K
 

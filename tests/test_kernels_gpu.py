@@ -188,6 +188,40 @@ def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine, h32):
     assert torch.equal(mr0, mr_fused[: mr0.numel()])
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,res", [(2, 16, 16, 256, 256, False), (1, 32, 48, 512, 512, False),
+                                                 (3, 16, 32, 128, 256, True), (1, 48, 16, 64, 512, True),
+                                                 (2, 8, 24, 256, 256, False)])
+def test_conv2d_up2_phases(B, H, W, Cin, Cout, res):
+    """Upsample2D's nearest ×2 + 3×3 conv as four 2×2 phase convs on the source grid
+    (rdmi_conv_args.w_up2, conv_halo_kernel MODE 3) against the fp32 conv of the upsampled input,
+    against the 9-tap form, with the epilogue's GroupNorm moments and per-image batch invariance.
+    (2, 8, 24): Ho = 16 is not a phase-tile multiple — the 9-tap form runs (bitwise check)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.randn(B, H, W, Cin, device=DEV, generator=g).half()
+    w = torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9)
+    wp, wu = K_.pack_conv(w, DEV), K_.pack_conv_up2(w, DEV)
+    b = torch.randn(Cout, device=DEV, generator=g) * 0.1
+    r = torch.randn(B, 2 * H, 2 * W, Cout, device=DEV, generator=g).half() if res else None
+    y = K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True, w_up2=wu)
+    y9 = K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True)
+    xin = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2.0, mode="nearest")
+    ref = F.conv2d(xin, w.half().float().to(DEV), b, padding=1)
+    if res:
+        ref = ref + r.float().permute(0, 3, 1, 2)
+    err, err9 = _rel(y.permute(0, 3, 1, 2), ref), _rel(y9.permute(0, 3, 1, 2), ref)
+    print(f"up2 B={B} {H}x{W} {Cin}->{Cout}: rel {err:.2e} (9-tap {err9:.2e})")
+    assert err < 4e-3
+    if (2 * H) % 32:
+        assert torch.equal(y, y9)
+    mr = K_.groupnorm_stats(y, 32, 1e-6)
+    assert torch.allclose(mr, K_.groupnorm_stats(y.clone(), 32, 1e-6), rtol=1e-5, atol=1e-6)
+    y0 = K_.conv2d(x[:1], wp, Cout, 3, upsample=True, bias=b, residual=None if r is None else r[:1], gn=True,
+                   w_up2=wu)
+    assert torch.equal(y0, y[:1])
+    assert torch.equal(K_.groupnorm_stats(y0, 32, 1e-6), mr[: 2 * 32])
+
+
 def test_groupnorm_moments_from_gemm(engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(12)

@@ -2,7 +2,8 @@
 every launch): per shape, time both settings alternately over several rounds and check that the
 outputs are bitwise identical (the switches change the schedule, not the K order).
 
-    python tools/conv_ab.py [--env RDMI_CONV_PIPE] [--rounds 3] [--iters 10]"""
+    python tools/conv_ab.py [--env RDMI_CONV_PIPE] [--rounds 3] [--iters 10]
+TF/s: the 9-tap algorithmic FLOPs (for RDMI_UP2 = 1 an effective rate: the phase form executes 4/9)."""
 import argparse
 import math
 import os
@@ -30,6 +31,8 @@ CASES = [
     ("vae 256 384^2 x8 full", 8, 384, 256, 256, False, "full"),
     ("vae 512 192^2 x8 plain", 8, 192, 512, 512, False, "plain"),
     ("vae up 256 384->768 x8", 8, 384, 256, 256, True, "plain"),
+    ("vae up 512 192->384 x8", 8, 192, 512, 512, True, "plain"),
+    ("vae up 512 96->192 x8", 8, 96, 512, 512, True, "plain"),
     ("unet 320 96^2 x48 full", 48, 96, 320, 320, False, "full"),
     ("unet 640 48^2 x48 full", 48, 48, 640, 640, False, "full"),
 ]
@@ -53,7 +56,9 @@ for lab, B, H, ci, co, up, var in CASES:
     if a.only and a.only not in lab:
         continue
     x = torch.randn(B, H, H, ci, device="cuda").half()
-    w = K.pack_conv(torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9), "cuda", ci)
+    w0 = torch.randn(co, ci, 3, 3) / math.sqrt(ci * 9)
+    w = K.pack_conv(w0, "cuda", ci)
+    wu = K.pack_conv_up2(w0, "cuda", ci) if up else None  # phase weights (RDMI_UP2 A/B)
     Ho = 2 * H if up else H
     res = torch.randn(B, Ho, Ho, co, device="cuda").half()
     gm, bt = 1 + 0.1 * torch.randn(ci, device="cuda"), 0.1 * torch.randn(ci, device="cuda")
@@ -67,7 +72,7 @@ for lab, B, H, ci, co, up, var in CASES:
     def run(v):
         os.environ[a.env] = v
         K.conv2d(x, w, co, 3, upsample=up, bias=bias, residual=res if var == "full" else None, out=outs[v],
-                 gn=var == "full", in_gn=ig)
+                 gn=var == "full", in_gn=ig, w_up2=wu)
 
     fl = 2.0 * B * Ho * Ho * co * ci * 9
     best = {v: 1e9 for v in vals}
