@@ -283,7 +283,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     """NHWC f16 conv.  x [B, H, W, Cin_pad]; w packed by pack_conv.  `pad` is symmetric; pad_tl
     overrides the top/left padding with bottom/right implied by out_hw (VAE Downsample2D).
     w_up2 (upsample only): pack_conv_up2's phase weights, which the library runs where its
-    phase-decomposed form applies (RDMI_UP2=0 turns it off).
+    phase-decomposed form applies — with RDMI_UP2=1 (opt-in; ignored otherwise).
     gn=True: also emit the output's GroupNorm moments (as gemm).
     in_gn=(mean_rstd, gamma, beta, groups, silu): GroupNorm(+SiLU) of x applied as it is read
     (rdmi.h rdmi_conv_args.in_*; only where conv2d_in_gn_supported)."""
@@ -322,8 +322,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
         return out
     if w.shape[1] < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
-    if w_up2 is not None and (f32 or os.environ.get("RDMI_UP2", "1") == "0"):
-        w_up2 = None
+    if w_up2 is not None and (f32 or os.environ.get("RDMI_UP2", "0") != "1"):
+        w_up2 = None  # opt-in: see DESIGN.md §7 (same accuracy in expectation, but the 768² depth
+        # parity sits on the min/max renormalisation of two pixels — tools/depth_sensitivity.py)
     if w_up2 is not None and (w_up2.dtype != F16 or tuple(w_up2.shape) != (4, cout, 4 * Cin) or
                               not w_up2.is_contiguous()):
         raise ValueError(f"conv2d: w_up2 must be pack_conv_up2's [4, {cout}, {4 * Cin}] f16")

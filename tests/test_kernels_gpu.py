@@ -191,12 +191,13 @@ def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine, h32):
 @pytest.mark.parametrize("B,H,W,Cin,Cout,res", [(2, 16, 16, 256, 256, False), (1, 32, 48, 512, 512, False),
                                                  (3, 16, 32, 128, 256, True), (1, 48, 16, 64, 512, True),
                                                  (2, 8, 24, 256, 256, False)])
-def test_conv2d_up2_phases(B, H, W, Cin, Cout, res):
+def test_conv2d_up2_phases(B, H, W, Cin, Cout, res, monkeypatch):
     """Upsample2D's nearest ×2 + 3×3 conv as four 2×2 phase convs on the source grid
     (rdmi_conv_args.w_up2, conv_halo_kernel MODE 3) against the fp32 conv of the upsampled input,
     against the 9-tap form, with the epilogue's GroupNorm moments and per-image batch invariance.
     (2, 8, 24): Ho = 16 is not a phase-tile multiple — the 9-tap form runs (bitwise check)."""
     K_ = _k()
+    monkeypatch.setenv("RDMI_UP2", "1")
     g = torch.Generator(device=DEV).manual_seed(13)
     x = torch.randn(B, H, W, Cin, device=DEV, generator=g).half()
     w = torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9)
@@ -205,6 +206,9 @@ def test_conv2d_up2_phases(B, H, W, Cin, Cout, res):
     r = torch.randn(B, 2 * H, 2 * W, Cout, device=DEV, generator=g).half() if res else None
     y = K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True, w_up2=wu)
     y9 = K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True)
+    monkeypatch.setenv("RDMI_UP2", "0")  # the default: phase weights given but not used
+    assert torch.equal(K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True, w_up2=wu), y9)
+    monkeypatch.setenv("RDMI_UP2", "1")
     xin = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2.0, mode="nearest")
     ref = F.conv2d(xin, w.half().float().to(DEV), b, padding=1)
     if res:
@@ -443,6 +447,7 @@ def test_attention_growing_max():
     """Key norms grow along the sequence so the row max rises by a few units per tile: the m̃
     re-set (and O/l rescale) fires repeatedly at moderate jumps, never at the first tile only."""
     K_ = _k()
+    monkeypatch.setenv("RDMI_UP2", "1")
     g = torch.Generator(device=DEV).manual_seed(13)
     B, S, H = 1, 1536, 2
     C = H * 64
@@ -496,6 +501,7 @@ def test_softmax_rows(cols, pad):
     """Row softmax (single-pass register kernel for cols % 4 == 0 and ≤ 16384, three-pass
     otherwise) against torch.softmax; the padding columns are written as zeros."""
     K_ = _k()
+    monkeypatch.setenv("RDMI_UP2", "1")
     g = torch.Generator(device=DEV).manual_seed(13)
     s = torch.randn(37, cols, device=DEV, generator=g) * 8
     out = torch.full((37, cols + pad), 7.0, device=DEV, dtype=torch.float16)
