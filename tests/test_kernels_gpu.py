@@ -447,7 +447,6 @@ def test_attention_growing_max():
     """Key norms grow along the sequence so the row max rises by a few units per tile: the m̃
     re-set (and O/l rescale) fires repeatedly at moderate jumps, never at the first tile only."""
     K_ = _k()
-    monkeypatch.setenv("RDMI_UP2", "1")
     g = torch.Generator(device=DEV).manual_seed(13)
     B, S, H = 1, 1536, 2
     C = H * 64
@@ -501,7 +500,6 @@ def test_softmax_rows(cols, pad):
     """Row softmax (single-pass register kernel for cols % 4 == 0 and ≤ 16384, three-pass
     otherwise) against torch.softmax; the padding columns are written as zeros."""
     K_ = _k()
-    monkeypatch.setenv("RDMI_UP2", "1")
     g = torch.Generator(device=DEV).manual_seed(13)
     s = torch.randn(37, cols, device=DEV, generator=g) * 8
     out = torch.full((37, cols + pad), 7.0, device=DEV, dtype=torch.float16)
