@@ -213,6 +213,11 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box: every rank on cuda:0, gloo collectives
+    # (the scaling runs themselves use one GPU per rank and RCCL)
+    shared = os.environ.get("RDMI_BENCH_SHARED_GPU") == "1"
+    if shared:
+        local = 0
 
     import torch
     import torch.distributed as dist
@@ -229,7 +234,10 @@ def main():
 
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
 
     from rollingdepth_amd import config as C
@@ -341,6 +349,8 @@ def main():
                        "parallelism": f"snippet-dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "validation": validation,
         }
+        if shared:
+            line["rehearsal"] = "RDMI_BENCH_SHARED_GPU=1: all ranks on one GPU over gloo (not a scaling number)"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
