@@ -61,8 +61,8 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
 
 __device__ __forceinline__ long chunk_lo(long P, int c) { return P * c / PS; }
 
-__global__ __launch_bounds__(256) void frame_stats(AlP p) {
-  const int f = blockIdx.x, c = blockIdx.y;
+// One (frame f, pixel chunk c) work unit of frame_stats; thread 0 returns the chunk's min/max of T.
+__device__ __forceinline__ void frame_stats_body(const AlP& p, int f, int c, float& mn_out, float& mx_out) {
   __shared__ double sh[8];
   double sa = 0.0, sd = 0.0;
   float mn = INFINITY, mx = -INFINITY;
@@ -107,8 +107,19 @@ __global__ __launch_bounds__(256) void frame_stats(AlP p) {
     double* o = p.fpart + ((long)f * PS + c) * 4;
     o[0] = A;
     o[1] = D;
-    o[2] = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
-    o[3] = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
+    mn_out = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
+    mx_out = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
+  }
+}
+
+__global__ __launch_bounds__(256) void frame_stats(AlP p) {
+  const int f = blockIdx.x, c = blockIdx.y;
+  float mn, mx;
+  frame_stats_body(p, f, c, mn, mx);
+  if (threadIdx.x == 0) {
+    double* o = p.fpart + ((long)f * PS + c) * 4;
+    o[2] = mn;
+    o[3] = mx;
   }
 }
 
@@ -123,9 +134,11 @@ __device__ __forceinline__ void frame_scales(const AlP& p, int f, float& sc, flo
   scd = (float)(D / (double)p.P);
 }
 
-__global__ __launch_bounds__(256) void snippet_grad(AlP p) {
-  const int gk = blockIdx.x;  // global snippet index
-  const int c = blockIdx.y;   // pixel chunk
+// One (global snippet gk, pixel chunk c) work unit of snippet_grad; the loss partials go to
+// l1o[gk·PS + c], l2o[gk·PS + c].  COHERENT: the gradient partials are stored as agent-scope atomics
+// (device-coherent, read by another workgroup in the same launch).
+template <bool COHERENT>
+__device__ __forceinline__ void snippet_grad_body(const AlP& p, int gk, int c, double* l1o, double* l2o) {
   const long p0 = chunk_lo(p.P, c), p1 = chunk_lo(p.P, c + 1);
   int d = 0;
   while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
@@ -164,29 +177,44 @@ __global__ __launch_bounds__(256) void snippet_grad(AlP p) {
   l2 = block_sum_d<256>(l2, sh);
   if (threadIdx.x == 0) {
     const long o = (long)gk * PS + c;
-    p.gs[o] = gs;
-    p.gt[o] = gt;
-    p.l1[o] = l1;
-    p.l2[o] = l2;
+    if (COHERENT) {
+      __hip_atomic_store(&p.gs[o], gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&p.gt[o], gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      p.gs[o] = gs;
+      p.gt[o] = gt;
+    }
+    l1o[o] = l1;
+    l2o[o] = l2;
   }
 }
 
-__global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) {
+__global__ __launch_bounds__(256) void snippet_grad(AlP p) {
+  snippet_grad_body<false>(p, blockIdx.x, blockIdx.y, p.l1, p.l2);
+}
+
+// Loss-history row of iteration `step` (the closure's loss.item(), summ.min(), summ.max(), :213) from
+// that iteration's loss partials l1/l2 [ntot·PS], chunk min/max mm(i) over N·PS chunks and the
+// parameters BEFORE its update (sflat = [s | t] by global snippet index, or NULL: p.s / p.t).
+template <typename MM>
+__device__ __forceinline__ void hist_row(const AlP& p, int step, double denom, const double* l1, const double* l2,
+                                         const float* sflat, MM mm) {
   __shared__ double sh[8];
-  // loss history (uses the parameters BEFORE this update, like the closure's loss)
   double L1 = 0.0, L2 = 0.0, soft = 0.0;
   for (int i = threadIdx.x; i < p.ntot * PS; i += 256) {
-    L1 += p.l1[i];
-    L2 += p.l2[i];
+    L1 += l1[i];
+    L2 += l2[i];
   }
   L1 = block_sum_d<256>(L1, sh);
   L2 = block_sum_d<256>(L2, sh);
   for (int d = 0; d < p.nd; ++d) {
     double a = 0.0, b = 0.0;
     for (int k = threadIdx.x; k < p.n[d]; k += 256) {
-      float r = fmaxf(0.f, 1.f - p.s[d][k]);
+      const float sv = sflat ? sflat[p.off[d] + k] : p.s[d][k];
+      const float tv = sflat ? sflat[p.ntot + p.off[d] + k] : p.t[d][k];
+      float r = fmaxf(0.f, 1.f - sv);
       a += (double)r * r;
-      b += (double)p.t[d][k] * p.t[d][k];
+      b += (double)tv * tv;
     }
     a = block_sum_d<256>(a, sh);
     b = block_sum_d<256>(b, sh);
@@ -194,8 +222,10 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
   }
   float mn = INFINITY, mx = -INFINITY;
   for (long i = threadIdx.x; i < (long)p.N * PS; i += 256) {
-    mn = fminf(mn, (float)p.fpart[i * 4 + 2]);
-    mx = fmaxf(mx, (float)p.fpart[i * 4 + 3]);
+    float lo, hi;
+    mm(i, lo, hi);
+    mn = fminf(mn, lo);
+    mx = fmaxf(mx, hi);
   }
   mn = wave_min(mn);
   mx = wave_max(mx);
@@ -205,7 +235,7 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
     rmm[1][threadIdx.x >> 6] = mx;
   }
   __syncthreads();
-  if (p.hist && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     mn = fminf(fminf(rmm[0][0], rmm[0][1]), fminf(rmm[0][2], rmm[0][3]));
     mx = fmaxf(fmaxf(rmm[1][0], rmm[1][1]), fmaxf(rmm[1][2], rmm[1][3]));
     float* h = p.hist + 3L * (step - 1);
@@ -214,6 +244,13 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
     h[2] = mx;
   }
   __syncthreads();
+}
+
+// torch.optim.Adam's update of parameter i (i < ntot: s of global snippet i, else t of i − ntot) at
+// iteration `step`, its gradient = Σ_c of the chunk partials (chunk order fixed) · loss_scale/numel +
+// the soft-constraint term.  Returns the parameter value before the update.
+template <bool COHERENT>
+__device__ __forceinline__ float adam_param(const AlP& p, int i, int step, double denom) {
   const double bc1 = 1.0 - pow((double)p.b1, (double)step);
   const double bc2 = 1.0 - pow((double)p.b2, (double)step);
   const float step_size = (float)(p.lr / bc1);
@@ -221,34 +258,99 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
   const float lw = 1.0f - p.b1;   // lerp weight (1 - beta1)
   const float vw = 1.0f - p.b2;   // addcmul value (1 - beta2)
   const float gscale = (float)(p.ls / denom);
-  for (int i = threadIdx.x; i < 2 * p.ntot; i += 256) {
-    const bool is_t = i >= p.ntot;
-    const int gk = is_t ? i - p.ntot : i;
-    int d = 0;
-    while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
-    const int k = gk - p.off[d];
-    float* prm = is_t ? &p.t[d][k] : &p.s[d][k];
-    const float pv = *prm;
-    const double* gp = (is_t ? p.gt : p.gs) + (long)gk * PS;
-    double gsum = 0.0;
-    for (int c = 0; c < PS; ++c) gsum += gp[c];
-    float g = (float)(gsum * (double)gscale);
-    const float nd = (float)p.n[d];
-    if (!is_t) {
-      float r = fmaxf(0.f, 1.f - pv);
-      g = addrn(g, mulrn(mulrn(mulrn(p.lmda2, 2.0f), r), -1.0f) / nd);
-    } else {
-      g = addrn(g, mulrn(mulrn(p.lmda3, 2.0f), pv) / nd);
-    }
-    float m = p.m[i], v = p.v[i];
-    const float diff = g - m;
-    m = (lw < 0.5f) ? addrn(m, mulrn(lw, diff)) : g - mulrn(diff, 1.0f - lw);
-    v = addrn(mulrn(v, p.b2), mulrn(mulrn(vw, g), g));
-    const float den = addrn(sqrtf(v) / bc2s, p.eps);
-    *prm = addrn(pv, mulrn(-step_size, m) / den);
-    p.m[i] = m;
-    p.v[i] = v;
+  const bool is_t = i >= p.ntot;
+  const int gk = is_t ? i - p.ntot : i;
+  int d = 0;
+  while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
+  const int k = gk - p.off[d];
+  float* prm = is_t ? &p.t[d][k] : &p.s[d][k];
+  const float pv = *prm;
+  const double* gp = (is_t ? p.gt : p.gs) + (long)gk * PS;
+  double gsum = 0.0;
+  for (int c = 0; c < PS; ++c)
+    gsum += COHERENT ? __hip_atomic_load(gp + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : gp[c];
+  float g = (float)(gsum * (double)gscale);
+  const float nd = (float)p.n[d];
+  if (!is_t) {
+    float r = fmaxf(0.f, 1.f - pv);
+    g = addrn(g, mulrn(mulrn(mulrn(p.lmda2, 2.0f), r), -1.0f) / nd);
+  } else {
+    g = addrn(g, mulrn(mulrn(p.lmda3, 2.0f), pv) / nd);
   }
+  float m = p.m[i], v = p.v[i];
+  const float diff = g - m;
+  m = (lw < 0.5f) ? addrn(m, mulrn(lw, diff)) : g - mulrn(diff, 1.0f - lw);
+  v = addrn(mulrn(v, p.b2), mulrn(mulrn(vw, g), g));
+  const float den = addrn(sqrtf(v) / bc2s, p.eps);
+  *prm = addrn(pv, mulrn(-step_size, m) / den);
+  p.m[i] = m;
+  p.v[i] = v;
+  return pv;
+}
+
+__global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) {
+  // loss history (uses the parameters BEFORE this update, like the closure's loss)
+  if (p.hist)
+    hist_row(p, step, denom, p.l1, p.l2, nullptr, [&](long i, float& lo, float& hi) {
+      lo = (float)p.fpart[i * 4 + 2];
+      hi = (float)p.fpart[i * 4 + 3];
+    });
+  for (int i = threadIdx.x; i < 2 * p.ntot; i += 256) adam_param<false>(p, i, step, denom);
+}
+
+// snippet_grad with Adam fused in (the default loop: two launches per iteration).  The workgroup
+// that finishes the LAST pixel chunk of snippet gk (a per-snippet arrival counter, agent-scope
+// release/acquire) applies Adam to s_gk and t_gk right there: their gradients need nothing else,
+// and every reader of s_gk, t_gk in this launch is one of those chunks.  The loss history is
+// deferred: the iteration's loss partials (hl), pre-update parameters (hst) and, in frame_stats,
+// chunk min/max (hmm) go to per-iteration slots and aligner_history turns them into rows once,
+// after the loop.  Same arithmetic in the same order as snippet_grad + adam_step: bitwise the
+// same results (tests/test_aligner_gpu.py::test_aligner_fused_loop_bitwise).
+__global__ __launch_bounds__(256) void snippet_grad_adam(AlP p, int it, double denom, unsigned* cnt, double* hl,
+                                                         float* hst) {
+  const long nps = (long)p.ntot * PS;
+  const int gk = blockIdx.x;
+  double* l1o = hl ? hl + (long)(it - 1) * 2 * nps : p.l1;
+  snippet_grad_body<true>(p, gk, blockIdx.y, l1o, l1o + nps);
+  // Hand-off without cache maintenance (an agent-scope fence writes back / invalidates the whole
+  // L2 — 1.6x slower over the loop): the partials were stored as device-coherent atomics by thread 0,
+  // which waits for them to complete before it arrives; the last arriver reads them the same way.
+  __shared__ unsigned last;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(&cnt[gk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PS - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x < 2) {
+    const int i = threadIdx.x ? p.ntot + gk : gk;
+    const float pv = adam_param<true>(p, i, it, denom);
+    if (hst) hst[(long)(it - 1) * 2 * p.ntot + i] = pv;
+  }
+  if (threadIdx.x == 0) cnt[gk] = 0u;  // re-armed for the next iteration (next launch)
+}
+
+__global__ __launch_bounds__(256) void frame_stats_hist(AlP p, float* hmm) {
+  const int f = blockIdx.x, c = blockIdx.y;
+  float mn, mx;
+  frame_stats_body(p, f, c, mn, mx);
+  if (hmm && threadIdx.x == 0) {
+    hmm[((long)f * PS + c) * 2] = mn;
+    hmm[((long)f * PS + c) * 2 + 1] = mx;
+  }
+}
+
+// History rows of the fused loop, one workgroup per iteration.
+__global__ __launch_bounds__(256) void aligner_history(AlP p, double denom, const double* hl, const float* hmm,
+                                                       const float* hst) {
+  const int it = blockIdx.x + 1;
+  const long nps = (long)p.ntot * PS, nfs = (long)p.N * PS;
+  const double* l1 = hl + (long)(it - 1) * 2 * nps;
+  const float* mm = hmm + (long)(it - 1) * nfs * 2;
+  hist_row(p, it, denom, l1, l1 + nps, hst + (long)(it - 1) * 2 * p.ntot, [&](long i, float& lo, float& hi) {
+    lo = mm[i * 2];
+    hi = mm[i * 2 + 1];
+  });
 }
 
 __global__ void zero_f32(float* x, long n) {
@@ -349,9 +451,20 @@ __global__ void prepare_k(PrepP p) {
   }
 }
 
-long ws_floats(int N, long P, int ntot) {
-  // 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v (2·ntot each)
-  return 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + 64;
+// Workspace (floats): 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v
+// (2·ntot each), the per-snippet arrival counters (ntot, padded to 8 B); with a history, the
+// fused loop's per-iteration slots: loss partials (2·ntot·PS doubles), chunk min/max (2·N·PS)
+// and pre-update parameters (2·ntot).
+long ws_floats(int N, long P, int ntot, int iters, bool hist) {
+  long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L);
+  if (hist) f += (long)iters * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
+  return f + 64;
+}
+
+// RDMI_ALIGNER_FUSED=0 selects the three-kernel loop (read per call: A/B and the bitwise test)
+bool fused_enabled() {
+  const char* e = getenv("RDMI_ALIGNER_FUSED");
+  return !(e && e[0] == '0');
 }
 
 }  // namespace
@@ -359,7 +472,7 @@ long ws_floats(int N, long P, int ntot) {
 extern "C" long rdmi_aligner_workspace(const rdmi_aligner_args* a) {
   int ntot = 0;
   for (int d = 0; d < a->n_dil; ++d) ntot += a->n[d];
-  return ws_floats(a->seq_len, a->P, ntot);
+  return ws_floats(a->seq_len, a->P, ntot, a->iters, a->history != nullptr);
 }
 
 extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
@@ -396,13 +509,34 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   p.Td = fw; fw += (long)p.N * p.P;
   p.m = fw; fw += 2 * ntot;
   p.v = fw; fw += 2 * ntot;
+  unsigned* cnt = (unsigned*)fw; fw += (ntot + 1) & ~1L;
   p.hist = a->history;
   int W = 0;
   for (int d = 0; d < p.nd; ++d) W += p.w;
   const double denom = (double)W * p.N * (double)p.P;  // numel of the [Σw, N, P] loss tensor
-  hipLaunchKernelGGL(zero_f32, dim3(16), dim3(256), 0, st, p.m, 4L * ntot);
+  hipLaunchKernelGGL(zero_f32, dim3(16), dim3(256), 0, st, p.m, 4L * ntot + ((ntot + 1) & ~1L));  // m, v, cnt
   int rc = rdmi::check_launch("aligner_zero");
   if (rc) return rc;
+  if (fused_enabled()) {
+    double* hl = nullptr;
+    float *hmm = nullptr, *hst = nullptr;
+    if (p.hist) {
+      hl = (double*)fw;
+      hmm = (float*)(hl + (long)a->iters * 2 * nps);
+      hst = hmm + (long)a->iters * 2 * p.N * PS;
+    }
+    for (int it = 1; it <= a->iters; ++it) {
+      hipLaunchKernelGGL(frame_stats_hist, dim3(p.N, PS), dim3(256), 0, st, p,
+                         hmm ? hmm + (long)(it - 1) * 2 * p.N * PS : nullptr);
+      hipLaunchKernelGGL(snippet_grad_adam, dim3(ntot, PS), dim3(256), 0, st, p, it, denom, cnt, hl, hst);
+      rc = rdmi::check_launch("aligner_iteration");
+      if (rc) return rc;
+    }
+    if (p.hist && a->iters > 0)
+      hipLaunchKernelGGL(aligner_history, dim3(a->iters), dim3(256), 0, st, p, denom, (const double*)hl,
+                         (const float*)hmm, (const float*)hst);
+    return rdmi::check_launch("aligner_history");
+  }
   for (int it = 1; it <= a->iters; ++it) {
     hipLaunchKernelGGL(frame_stats, dim3(p.N, PS), dim3(256), 0, st, p);
     hipLaunchKernelGGL(snippet_grad, dim3(ntot, PS), dim3(256), 0, st, p);

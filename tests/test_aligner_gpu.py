@@ -85,3 +85,32 @@ def test_aligner_merge_f16_rounding():
                           dil, N, shift)
     got = out.half().float().cpu().numpy()
     assert np.abs(got - ref[:, 0].astype(np.float32)).max() <= 2e-3
+
+
+@pytest.mark.parametrize("case", ["small", "metric"])
+def test_aligner_fused_loop_bitwise(case, monkeypatch):
+    """The two-launch iteration (aligner.hip snippet_grad_adam: per-snippet last-chunk Adam, deferred
+    loss history) gives bitwise the scales, translations, loss history and merged depth of the
+    three-kernel loop (RDMI_ALIGNER_FUSED=0).  'metric': the fast preset's aligner shape
+    (N = 100 frames, dilations [1, 25], P = 5 929 subsampled pixels of a 768² frame), 300 iterations."""
+    from rollingdepth_amd.aligner import DepthAligner
+
+    if case == "small":
+        snips, dil = _synth()
+        iters = 120
+    else:
+        snips, dil = _synth(N=100, dil=(1, 25), H=774, W=774)  # (774 − 4) / 10 → 77² = 5 929 px
+        iters = 300
+    xs = [torch.from_numpy(x).to(DEV) for x in snips]
+    outs = {}
+    for coop in ("1", "0"):
+        monkeypatch.setenv("RDMI_ALIGNER_FUSED", coop)
+        al = DepthAligner(device=torch.device(DEV), num_iterations=iters)
+        m, s, t, h = al.run(xs, list(dil))
+        torch.cuda.synchronize()
+        outs[coop] = (m.cpu(), [v.cpu() for v in s], [v.cpu() for v in t], h)
+    a, b = outs["1"], outs["0"]
+    assert torch.equal(a[0], b[0])
+    for d in range(len(dil)):
+        assert torch.equal(a[1][d], b[1][d]) and torch.equal(a[2][d], b[2][d])
+    assert a[3] == b[3]
