@@ -98,3 +98,36 @@ def write_video_from_numpy(frames: np.ndarray, output_path, fps: int = 30, codec
     except ImportError as e:
         raise ImportError("video encoding needs PyAV, which is not installed in this image") from e
     raise NotImplementedError("video encoding (PyAV present but not wired in this build)")  # pragma: no cover
+
+
+def get_video_fps(video_path) -> float:
+    """video_io.py:211-224 — reading the container needs PyAV (absent from this image)."""
+    try:
+        import av
+    except ImportError as e:
+        raise ImportError("get_video_fps needs PyAV, which is not installed in this image") from e
+    container = av.open(video_path)  # pragma: no cover — PyAV absent here
+    try:
+        return float(container.streams.video[0].average_rate)
+    finally:
+        container.close()
+
+
+def concatenate_videos_horizontally_torch(video1, video2, gap: int = 0, gap_color=None) -> torch.Tensor:
+    """video_io.py:227-265: video2 resized (antialiased bilinear, rdmi_resize) to video1's [H1, W1] and
+    concatenated to its right along the width.  As in the reference, the gap strip is built but the
+    returned tensor is the concatenation WITHOUT it (:259-263 overwrite the gapped result), so `gap`
+    and `gap_color` do not change the output.  [N, 3, H, W] numpy or torch, float or uint8; a host
+    tensor is resized on the default device and returned on the host.  uint8 frames are resized in
+    f32 and rounded half-to-even (torchvision's float path for uint8 tensors)."""
+    if isinstance(video1, np.ndarray):
+        video1 = torch.from_numpy(video1)
+    if isinstance(video2, np.ndarray):
+        video2 = torch.from_numpy(video2)
+    N, C, H1, W1 = video1.shape
+    dev = video2.device if video2.is_cuda else torch.device("cuda")
+    r = K.resize(video2.to(dev), (H1, W1), "BILINEAR")
+    if video2.dtype == torch.uint8:
+        r = r.round_().clamp_(0, 255)
+    r = r.to(video1.dtype)
+    return torch.cat([video1, r.to(video1.device)], dim=3)

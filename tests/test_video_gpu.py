@@ -118,3 +118,28 @@ def test_call_with_decoded_frames_and_restore_res():
     d = (out.depth_pred.float() - want).abs().max().item()
     print(f"restore_res depth max |d| {d:.2e}")
     assert d <= 2e-3, d  # f16 storage of the restored map
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.uint8])
+def test_concatenate_videos_horizontally(dtype):
+    """video_io.py:227-265: video2 resized to video1's size (antialiased bilinear) and appended along
+    the width; the gap argument does not change the result (the reference overwrites the gapped cat)."""
+    import torch.nn.functional as F
+
+    from rollingdepth_amd.video_io import concatenate_videos_horizontally_torch
+
+    g = torch.Generator().manual_seed(5)
+    v1 = torch.rand(2, 3, 48, 64, generator=g) * 255
+    v2 = torch.rand(2, 3, 100, 90, generator=g) * 255
+    if dtype == torch.uint8:
+        v1, v2 = v1.to(torch.uint8), v2.to(torch.uint8)
+    out = concatenate_videos_horizontally_torch(v1, v2, gap=10)
+    ref2 = F.interpolate(v2.float().cuda(), size=(48, 64), mode="bilinear", align_corners=False, antialias=True)
+    if dtype == torch.uint8:
+        ref2 = ref2.round().clamp(0, 255)
+    ref = torch.cat([v1, ref2.to(dtype).cpu()], dim=3)
+    assert out.shape == (2, 3, 48, 128) and out.dtype == dtype and out.device == v1.device
+    if dtype == torch.uint8:
+        assert (out.int() - ref.int()).abs().max().item() <= 1
+    else:
+        assert (out - ref).abs().max().item() <= 1e-3
