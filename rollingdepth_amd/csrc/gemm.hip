@@ -47,6 +47,83 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 constexpr unsigned OOB = 0x80000000u;  // byte offset past every descriptor's extent → zeros
 
+// GroupNorm(+SiLU)-transformed halo values → f16 with the conv's zero padding: out-of-image pixels
+// (in = false) become 0.  Pairs rounded by one v_cvt_pk_f16_f32 (RNE, as the scalar conversions) and
+// the padding applied to the packed word, only in waves that hold such a pixel: the same bits as
+// `in ? (f16)f : 0` per element, 1.5 fewer VALU per element.
+__device__ __forceinline__ f16x4 gn_pack4(const float* f, bool in) {
+  unsigned w0, w1;
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(w0) : "v"(f[0]), "v"(f[1]));
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(w1) : "v"(f[2]), "v"(f[3]));
+  if (!__all(in)) {
+    w0 = in ? w0 : 0u;
+    w1 = in ? w1 : 0u;
+  }
+  return __builtin_bit_cast(f16x4, (__attribute__((ext_vector_type(2))) unsigned){w0, w1});
+}
+
+// GroupNorm of one f16 halo value (the low or high half of w): fmaf((float)v, sc, sh) as one
+// v_fma_mix_f32 (the f16 operand converted exactly; written as asm so that hipcc does not SLP-pack the
+// affine into v_pk_fma_f32, slower beside MFMAs).
+template <bool HI>
+__device__ __forceinline__ float gn_elem(unsigned w, float sc, float sh) {
+  float f;
+  if (HI)
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(f) : "v"(w), "v"(sc), "v"(sh));
+  else
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(f) : "v"(w), "v"(sc), "v"(sh));
+  return f;
+}
+
+// silu_f of four values: x · rcp(1 + exp2(x · −log2 e)), the same instructions as silu_f.  One asm
+// block so that every v_exp / v_rcp result is read three instructions later (the trans-result
+// forwarding hazard that hipcc pads for its own instructions does not see inside inline asm).
+__device__ __forceinline__ void silu4(float (&f)[4]) {
+  float t0, t1, t2, t3;
+  asm("v_mul_f32 %0, 0xbfb8aa3b, %4\n\t"
+      "v_mul_f32 %1, 0xbfb8aa3b, %5\n\t"
+      "v_mul_f32 %2, 0xbfb8aa3b, %6\n\t"
+      "v_mul_f32 %3, 0xbfb8aa3b, %7\n\t"
+      "v_exp_f32 %0, %0\n\t"
+      "v_exp_f32 %1, %1\n\t"
+      "v_exp_f32 %2, %2\n\t"
+      "v_exp_f32 %3, %3\n\t"
+      "v_add_f32 %0, 1.0, %0\n\t"
+      "v_add_f32 %1, 1.0, %1\n\t"
+      "v_add_f32 %2, 1.0, %2\n\t"
+      "v_add_f32 %3, 1.0, %3\n\t"
+      "v_rcp_f32 %0, %0\n\t"
+      "v_rcp_f32 %1, %1\n\t"
+      "v_rcp_f32 %2, %2\n\t"
+      "v_rcp_f32 %3, %3\n\t"
+      "v_mul_f32 %0, %4, %0\n\t"
+      "v_mul_f32 %1, %5, %1\n\t"
+      "v_mul_f32 %2, %6, %2\n\t"
+      "v_mul_f32 %3, %7, %3"
+      : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+      : "v"(f[0]), "v"(f[1]), "v"(f[2]), "v"(f[3]));
+  f[0] = t0;
+  f[1] = t1;
+  f[2] = t2;
+  f[3] = t3;
+}
+
+// n (multiple of 4) halo values in place: GroupNorm (+SiLU), f16, zero padding where !in
+template <int NW, bool SILU>
+__device__ __forceinline__ void gn_xform_words(unsigned (&w)[NW], const float* sc, const float* sh, bool in) {
+#pragma unroll
+  for (int j = 0; j < NW; j += 2) {
+    float f[4] = {gn_elem<false>(w[j], sc[2 * j], sh[2 * j]), gn_elem<true>(w[j], sc[2 * j + 1], sh[2 * j + 1]),
+                  gn_elem<false>(w[j + 1], sc[2 * j + 2], sh[2 * j + 2]),
+                  gn_elem<true>(w[j + 1], sc[2 * j + 3], sh[2 * j + 3])};
+    if (SILU) silu4(f);
+    const f16x4 o = gn_pack4(f, in);
+    const auto u = __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o);
+    w[j] = u[0];
+    w[j + 1] = u[1];
+  }
+}
+
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f16* l) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, 0, 0, 0);
 }
@@ -924,16 +1001,15 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     f16* lh = lds + (cbn & 1) * HALO + (wid + 8 * e) * 8 * BKP + lane * 8 + hf * 4;
     const float* ts = gnt + cbn * 64 + chunk * 8 + hf * 4;
     const f32x4 sc = *(const f32x4*)ts, sh = *(const f32x4*)(ts + GNT);
-    const f16x4 v = *(const f16x4*)lh;
+    unsigned w[2];
+    *(f16x4*)w = *(const f16x4*)lh;
     const bool in = hoff[e] >= 0;
-    f16x4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float f = fmaf((float)v[i], sc[i], sh[i]);
-      if (p.gsilu) f = silu_f(f);
-      o[i] = in ? (f16)f : (f16)0.f;
-    }
-    *(f16x4*)lh = o;
+    const float scv[4] = {sc[0], sc[1], sc[2], sc[3]}, shv[4] = {sh[0], sh[1], sh[2], sh[3]};
+    if (p.gsilu)  // the SiLU flag dispatched once per piece, not tested per element
+      gn_xform_words<2, true>(w, scv, shv, in);
+    else
+      gn_xform_words<2, false>(w, scv, shv, in);
+    *(f16x4*)lh = *(const f16x4*)w;
   };
 
   // prologue: halo(0) and the weights of K-tiles 0 and 1; wait for halo(0) + B(0)
@@ -1217,16 +1293,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     for (int e = 0; e < HPW; ++e)
       if (hv(e)) {
         f16* lh = lds + (wid + 4 * e) * 8 * BKP + lane * 8;
-        const f16x8 v = *(const f16x8*)lh;
+        unsigned w[4];
+        *(f16x8*)w = *(const f16x8*)lh;
         const bool in = hoff[e] >= 0;
-        f16x8 o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float f = fmaf((float)v[i], sc[i], sh[i]);
-          if (p.gsilu) f = silu_f(f);
-          o[i] = in ? (f16)f : (f16)0.f;
-        }
-        *(f16x8*)lh = o;
+        if (p.gsilu)  // the SiLU flag dispatched once per piece (see gn_elem)
+          gn_xform_words<4, true>(w, sc, sh, in);
+        else
+          gn_xform_words<4, false>(w, sc, sh, in);
+        *(f16x8*)lh = *(const f16x8*)w;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
