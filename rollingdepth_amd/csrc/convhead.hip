@@ -66,11 +66,25 @@ __global__ __launch_bounds__(HT) void head_taps(const T* __restrict__ x, long HW
 // normalising and weighting 8 channels, so one wave load instruction reads 64/LPP whole pixel
 // rows (the per-thread form above reads 64 rows 2·C bytes apart per instruction); the 9 tap sums
 // are reduced across the LPP lanes in a fixed butterfly and written pixel-major, d[p][9].
-template <typename T, int LPP>
+// Sum over the LPP (≤ 16) lanes of a row group in the order of the xor butterfly (xor 1, 2, 4, 8): the
+// partner value comes by DPP (quad_perm for 1 and 2, row_half_mirror / row_mirror for 4 and 8 — at
+// those levels every lane of the partner group holds the same partial, so lane 7 − i / 15 − i gives
+// the same operand as lane i ^ 4 / i ^ 8): bitwise the __shfl_xor form, without the LDS round trips
+// of ds_bpermute.
+template <int LPP>
+__device__ __forceinline__ float group_sum(float v) {
+  if (LPP > 1) v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  if (LPP > 2) v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  if (LPP > 4) v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  if (LPP > 8) v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+template <typename T, int LPP, bool SILU>
 __global__ __launch_bounds__(HT) void head_taps_v(const T* __restrict__ x, long HW, int G,
                                                   const float* __restrict__ mr, const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, const float* __restrict__ w,
-                                                  int silu, float* __restrict__ d, long P, int ppb) {
+                                                  float* __restrict__ d, long P, int ppb) {
   constexpr int C = 8 * LPP;
   const int b = blockIdx.y;
   const int cl = threadIdx.x % LPP;  // channel chunk of this lane
@@ -97,14 +111,19 @@ __global__ __launch_bounds__(HT) void head_taps_v(const T* __restrict__ x, long 
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float f = fmaf(v[e], sc[e], sh[e]);
-      if (silu) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
+      if constexpr (SILU) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
 #pragma unroll
       for (int t = 0; t < 9; ++t) acc[t] = fmaf(f, wt[t][e], acc[t]);
     }
+    if constexpr (LPP <= 16) {
 #pragma unroll
-    for (int o = 1; o < LPP; o <<= 1)
+      for (int t = 0; t < 9; ++t) acc[t] = group_sum<LPP>(acc[t]);
+    } else {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) acc[t] += __shfl_xor(acc[t], o, 64);
+      for (int o = 1; o < LPP; o <<= 1)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] += __shfl_xor(acc[t], o, 64);
+    }
     float* dp = d + ((long)b * HW + p) * 9;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -172,8 +191,12 @@ int head_launch(const void* x, int B, int H, int W, int C, int G, const float* m
     dim3 g(rdmi::div_up(HW, PPB), B);
 #define RDMI_HEAD(L)                                                                                             \
   case L:                                                                                                        \
-    hipLaunchKernelGGL((head_taps_v<T, L>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma, beta, w,   \
-                       silu, workspace, P, PPB);                                                                 \
+    if (silu)                                                                                                    \
+      hipLaunchKernelGGL((head_taps_v<T, L, true>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma,    \
+                         beta, w, workspace, P, PPB);                                                            \
+    else                                                                                                         \
+      hipLaunchKernelGGL((head_taps_v<T, L, false>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma,   \
+                         beta, w, workspace, P, PPB);                                                            \
     break;
     switch (lpp) {
       RDMI_HEAD(1) RDMI_HEAD(2) RDMI_HEAD(4) RDMI_HEAD(8) RDMI_HEAD(16) RDMI_HEAD(32) RDMI_HEAD(64)
