@@ -200,7 +200,7 @@ __device__ __forceinline__ int col_base(bool perm, int nw, int j, int fq) {
   return perm ? nw + 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : nw + j * 16 + fq * 4;
 }
 
-template <int RM, int RN, int WTN, bool SILU, class Rows>
+template <int RM, int RN, int WTN, bool SILU, class Rows, bool GELUX = false>
 __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
                                              int fr, int fq, bool perm) {
   const long cb = (long)bz * p.sC;
@@ -394,7 +394,10 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
         for (int r = 0; r < 4; ++r) {
           const float h = acc[i][j][r] * p.alpha + bh[j][r];
           const float g = acc[i][j + RN / 2][r] * p.alpha + bg[j][r];
-          v[r] = h * (p.gelu_exact ? gelu_erf(g) : gelu_erf_fast(g));
+          if constexpr (GELUX)
+            v[r] = h * gelu_erf(g);
+          else
+            v[r] = h * gelu_erf_fast(g);  // the exact-erf flag dispatched at launch (store_tile), not per element
           if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
         }
         if (p.c_f32) {
@@ -416,6 +419,12 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
 template <int RM, int RN, int WTN, class Rows>
 __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
                                            int fr, int fq, bool perm = false) {
+  if constexpr (WTN == 64) {  // only these tiles carry the GEGLU epilogue (RDMI_GELU_EXACT A/B)
+    if (p.gelu_exact) {
+      store_tile_t<RM, RN, WTN, false, Rows, true>(p, acc, rows, nw, bz, fr, fq, perm);
+      return;
+    }
+  }
   if (p.silu)
     store_tile_t<RM, RN, WTN, true>(p, acc, rows, nw, bz, fr, fq, perm);
   else
