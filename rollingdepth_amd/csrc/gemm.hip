@@ -35,7 +35,6 @@ struct GemmP {
   // GroupNorm (+SiLU) of the conv INPUT, applied as it is read (conv_halo_kernel<..., GN = true>)
   const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
   int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
-  int gelu_exact;  // GEGLU through ocml erff instead of gelu_erf_fast (RDMI_GELU_EXACT=1, A/B)
   int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
 };
 
@@ -200,7 +199,7 @@ __device__ __forceinline__ int col_base(bool perm, int nw, int j, int fq) {
   return perm ? nw + 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : nw + j * 16 + fq * 4;
 }
 
-template <int RM, int RN, int WTN, bool SILU, class Rows, bool GELUX = false>
+template <int RM, int RN, int WTN, bool SILU, class Rows>
 __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
                                              int fr, int fq, bool perm) {
   const long cb = (long)bz * p.sC;
@@ -394,10 +393,7 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
         for (int r = 0; r < 4; ++r) {
           const float h = acc[i][j][r] * p.alpha + bh[j][r];
           const float g = acc[i][j + RN / 2][r] * p.alpha + bg[j][r];
-          if constexpr (GELUX)
-            v[r] = h * gelu_erf(g);
-          else
-            v[r] = h * gelu_erf_fast(g);  // the exact-erf flag dispatched at launch (store_tile), not per element
+          v[r] = h * gelu_erf_fast(g);  // no per-element flag: hipcc would branch on it per output
           if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
         }
         if (p.c_f32) {
@@ -419,12 +415,6 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
 template <int RM, int RN, int WTN, class Rows>
 __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
                                            int fr, int fq, bool perm = false) {
-  if constexpr (WTN == 64) {  // only these tiles carry the GEGLU epilogue (RDMI_GELU_EXACT A/B)
-    if (p.gelu_exact) {
-      store_tile_t<RM, RN, WTN, false, Rows, true>(p, acc, rows, nw, bz, fr, fq, perm);
-      return;
-    }
-  }
   if (p.silu)
     store_tile_t<RM, RN, WTN, true>(p, acc, rows, nw, bz, fr, fq, perm);
   else
@@ -2036,10 +2026,6 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   p.alpha = a->alpha;
   p.M = a->M; p.N = a->N; p.K = (a->K + BK - 1) / BK * BK; p.Kvalid = a->K;
   p.geglu = a->epilogue == RDMI_EPI_GEGLU;
-  if (p.geglu) {
-    const char* ge = getenv("RDMI_GELU_EXACT");
-    p.gelu_exact = ge && ge[0] == '1';
-  }
   p.silu = a->epilogue == RDMI_EPI_SILU;
   p.vec = vec_ok(p);
   RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm: GEGLU output needs 4-element aligned rows");

@@ -2,7 +2,8 @@
 the same forward under build switches that only change f16 rounding (phase-decomposed upsample
 conv, flash vs GEMM VAE mid attention, 32×32×16 conv form, exact-erf GEGLU), reporting the decoded-snippet error (before the
 aligner) and the co-aligned depth error (after the aligner's 2000 sign-driven Adam steps and the
-min/max renormalisation) against the reference.
+min/max renormalisation) against the reference.  (The exact-erf GEGLU switch, RDMI_GELU_EXACT, was
+removed after the study recorded in profiles/r02_v28_depth_sens3.log; it is ignored now.)
 
     python tools/depth_sensitivity.py [fixture]"""
 import itertools
