@@ -209,3 +209,26 @@ def test_video_target_size_and_missing_pyav():
             V.write_video_from_numpy(np.zeros((1, 4, 4, 3), np.uint8), "/tmp/x.mp4")
     with pytest.raises(ValueError):
         V.frames_from_rgb24(np.zeros((1, 4, 4, 4), np.uint8))
+
+
+def test_aligner_workspace_sizes_history_slots():
+    """rdmi_aligner_workspace (host-only, no GPU): the fused aligner loop keeps per-iteration loss
+    partials (2·ntot·PS doubles), chunk min/max (2·N·PS floats) and pre-update parameters (2·ntot)
+    when a history is requested, and nothing per iteration without one (aligner.hip ws_floats)."""
+    import ctypes as C
+
+    from rollingdepth_amd import _native
+
+    a = _native.AlignerArgs()
+    a.n_dil, a.w, a.seq_len, a.P = 2, 3, 100, 5929
+    a.n[0], a.n[1] = 98, 48
+    ntot, PS = 146, 8
+    a.iters = 2000
+    a.history = None
+    base = _native.lib.rdmi_aligner_workspace(C.byref(a))
+    assert base >= 8 * ntot * PS + 8 * 100 * PS + 2 * 100 * 5929 + 4 * ntot + ntot
+    a.history = 1  # any non-null pointer: the size depends only on its presence
+    with_hist = _native.lib.rdmi_aligner_workspace(C.byref(a))
+    assert with_hist - base >= 2000 * (4 * ntot * PS + 2 * 100 * PS + 2 * ntot)
+    a.iters = 10
+    assert _native.lib.rdmi_aligner_workspace(C.byref(a)) < with_hist
