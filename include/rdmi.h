@@ -143,14 +143,16 @@ int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, long HW, int 
 
 /* GroupNorm apply (+ SiLU when silu = 1) fused with a 3×3, stride-1, pad-1 convolution to ONE output
  * channel: y[b, h, w] = bias + Σ_{dy,dx,c} w[3dy+dx][c] · n(x)[b, h+dy-1, w+dx-1, c], n = the
- * normalised (+SiLU) input, zero outside the image.  x [B][H][W][C] and y [B][H][W] in `dtype`
- * (RDMI_F16 / RDMI_F32), w [9][C] f32, workspace ≥ rdmi_conv3x3_to1_gn_workspace(B, H, W) floats.  Replaces the decoder's
+ * normalised (+SiLU) input, zero outside the image.  x [B][H][W][C] in `dtype` (RDMI_F16 / RDMI_F32),
+ * y [B][H][W] in `y_dtype` (RDMI_F16 / RDMI_F32: the f16 pipeline keeps its decoded depth in f32, so
+ * the f16 rounding of the depth map does not reach the aligner and the min/max renormalisation),
+ * w [9][C] f32, workspace ≥ rdmi_conv3x3_to1_gn_workspace(B, H, W) floats.  Replaces the decoder's
  * conv_norm_out → conv_act → conv_out (vae.py:335-347) followed by the depth pipeline's mean over
  * the RGB outputs (rollingdepth_pipeline.py:737), which is linear and folded into w / bias. */
 long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W);
 int rdmi_conv3x3_to1_gn(const void* x, int dtype, int B, int H, int W, int C, int G, const float* mean_rstd,
                         const float* gamma, const float* beta, int silu, const float* w, float bias,
-                        void* y, float* workspace, void* stream);
+                        void* y, int y_dtype, float* workspace, void* stream);
 
 /* LayerNorm over the last dim (BasicTransformerBlock.norm1/2/3, attention.py:445,495,522). */
 int rdmi_layernorm(const void* x, void* y, int dtype, long M, int C, const float* gamma, const float* beta,
@@ -256,15 +258,19 @@ int rdmi_renormalize_f32(float* x, long n, const float* minmax, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * DepthAligner (rollingdepth/depth_aligner.py) — co-alignment of dilated snippets.
- * Snippet layout: one f32 buffer per dilation, x_d [n_d][w][P] (border-cropped, stride-subsampled,
- * min-shifted; depth_aligner.py:78-92).  Parameters s_d, t_d are f32 [n_d].
+ * Snippet layout: one f32 buffer per dilation, x_d [n_d][w_d][P] (border-cropped, stride-subsampled,
+ * min-shifted; depth_aligner.py:78-92).  Parameters s_d, t_d are f32 [n_d].  Snippet lengths w_d may
+ * differ per dilation (rollingdepth_pipeline.py:221-226): the loss then follows the reference's
+ * scatter of dilation i's slot j into row i·w_i + j of [Σw, N, P] (depth_aligner.py:169-188) —
+ * coinciding rows are overwritten by the later dilation, and a layout whose rows run past Σw
+ * (the reference's IndexError) is rejected with RDMI_E_ARG.
  */
 typedef struct rdmi_aligner_args {
   int n_dil;                 /* number of dilations (≤ 8) */
-  const float* x[8];         /* subsampled snippets per dilation [n_d][w][P] */
+  const float* x[8];         /* subsampled snippets per dilation [n_d][w_d][P] */
   float* s[8]; float* t[8];  /* scales / translations [n_d] (in: init, out: result) */
   int n[8]; int stride[8];   /* snippets per dilation, frame stride (dilation) */
-  int w;                     /* snippet length (all dilations) */
+  int w[8];                  /* snippet length per dilation (Σ w_d ≤ 64) */
   int seq_len; long P;
   float lr, beta1, beta2, eps, lmda2, lmda3, depth_w, loss_scale;
   int iters;
@@ -278,26 +284,27 @@ int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream);
  * x [n][w][H][W] (f16/f32) → out [n][w][P] f32 with out = dtype(x - shift[0]) (:78-92). */
 int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int H, int W, int border,
                          int factor, const float* shift, float* out, void* stream);
-/* merge_scaled_triplets (:231-262): full-resolution snippets per dilation xf_d [n_d][w][HW]
+/* merge_scaled_triplets (:231-262): full-resolution snippets per dilation xf_d [n_d][w_d][HW]
+ * (w: snippet length per dilation)
  * (x_f32 = 1: f32 snippets; 0: f16 snippets in the reference's f16 arithmetic; 2: f16 snippets with
  * the shift and s·x+t in f32 — no intermediate f16 rounding; the min shift read from shift[0] is
  * applied first),
  * s/t f32 → out [seq_len][HW] f32 (s·x+t rounded through the snippet dtype exactly where the
  * reference computes in it; the per-frame mean is accumulated in f32). */
 int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
-                       const float* const* t, const int* n, const int* stride, int w, int seq_len,
+                       const float* const* t, const int* n, const int* stride, const int* w, int seq_len,
                        long HW, const float* shift, float* out, void* stream);
 
 /* Sharded merge: each rank sums s·x+t of ITS full-resolution snippets — rows
- * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w][HW] — into sum_out [seq_len][HW] f32 (the
+ * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w_d][HW] — into sum_out [seq_len][HW] f32 (the
  * same per-slot arithmetic as rdmi_aligner_merge, zero where no local slot covers a frame); after a
  * reduce-scatter SUM by frame, rdmi_aligner_merge_finish divides frames f0 .. f0+nf-1 by their cover
  * count over all n[d] snippets.  World size 1 reproduces rdmi_aligner_merge bitwise. */
 int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                const float* const* t, const int* n, const int* stride, const int* k0,
-                               const int* nloc, int w, int seq_len, long HW, const float* shift, float* sum_out,
+                               const int* nloc, const int* w, int seq_len, long HW, const float* shift, float* sum_out,
                                void* stream);
-int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w, int f0, int nf, long HW,
+int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf, long HW,
                               const float* sum, float* out, void* stream);
 
 /* Single-head flash attention for head dim 512 (f16): the VAE mid-block attention

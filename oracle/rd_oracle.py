@@ -333,8 +333,12 @@ def aligner_optimize(xs: Sequence[np.ndarray], idx: Sequence[np.ndarray], seq_le
                      betas=(0.5, 0.9), eps=1e-8, history=True):
     """DepthAligner.optimize (depth_aligner.py:123-229) restated with explicit gradients.
 
-    xs[d]:  [n_d, w, P] float32 subsampled, min-shifted snippets of dilation d.
-    idx[d]: [n_d, w] frame index of (snippet, slot).
+    xs[d]:  [n_d, w_d, P] float32 subsampled, min-shifted snippets of dilation d.
+    idx[d]: [n_d, w_d] frame index of (snippet, slot).
+    Row layout (depth_aligner.py:179-188): slot j of dilation d is row d·w_d + j of the [Σw, N, P]
+    tensors; when snippet lengths differ, rows of different dilations can coincide and the later
+    dilation's value overwrites the earlier one's at the frames both cover (`alive` below: an
+    overwritten slot contributes neither to the frame means, the count B, the loss nor the gradient).
     Loss = loss_scale·(mean|M−T|·B/s + w_d·mean|M_d−T_d|·B/s_d) + Σ_d λ2·mean(relu(1−s)²) + λ3·mean(t²)
     where the means run over the FULL Σw×N×P tensors (zeros included, :200-201), T/T_d are the
     detached per-frame means (:190-198), M_d = 1/clip(A, 1e-3) (:182-184), A = x·s + t.
@@ -343,8 +347,18 @@ def aligner_optimize(xs: Sequence[np.ndarray], idx: Sequence[np.ndarray], seq_le
     """
     nd = len(xs)
     P = xs[0].shape[-1]
-    R = sum(x.shape[1] for x in xs)
+    ws = [x.shape[1] for x in xs]
+    R = sum(ws)
+    rb = [d * w for d, w in enumerate(ws)]
     denom = np.float32(R * seq_len * P)
+    alive = [np.ones(ix.shape, bool) for ix in idx]
+    for d in range(nd):
+        for j in range(ws[d]):
+            r = rb[d] + j
+            for d2 in range(d + 1, nd):
+                j2 = r - rb[d2]
+                if 0 <= j2 < ws[d2]:
+                    alive[d][:, j] &= ~np.isin(idx[d][:, j], idx[d2][:, j2])
     s = [np.ones(x.shape[0], np.float32) for x in xs]
     t = [np.zeros(x.shape[0], np.float32) for x in xs]
     params = s + t
@@ -352,8 +366,8 @@ def aligner_optimize(xs: Sequence[np.ndarray], idx: Sequence[np.ndarray], seq_le
     v = [np.zeros_like(p) for p in params]
     b1, b2 = _f32(betas[0]), _f32(betas[1])
     cnt = np.zeros(seq_len, np.float32)
-    for ix in idx:
-        np.add.at(cnt, ix.reshape(-1), 1.0)
+    for ix, al in zip(idx, alive):
+        np.add.at(cnt, ix[al], 1.0)
     hist = []
     for it in range(iters):
         A = [x * s[d][:, None, None] + t[d][:, None, None] for d, x in enumerate(xs)]  # mul then add
@@ -361,10 +375,13 @@ def aligner_optimize(xs: Sequence[np.ndarray], idx: Sequence[np.ndarray], seq_le
         Ad = [_f32(1.0) / a for a in Ac]
         summ = np.zeros((seq_len, P), np.float32)
         summd = np.zeros((seq_len, P), np.float32)
-        for d in range(nd):  # row order of M: dilation, then slot (depth_aligner.py:179-188)
-            for j in range(xs[d].shape[1]):
-                summ[idx[d][:, j]] += A[d][:, j]
-                summd[idx[d][:, j]] += Ad[d][:, j]
+        for r in range(R):  # row order of M (depth_aligner.py:179-190)
+            for d in range(nd):
+                j = r - rb[d]
+                if 0 <= j < ws[d]:
+                    al = alive[d][:, j]
+                    summ[idx[d][al, j]] += A[d][al, j]
+                    summd[idx[d][al, j]] += Ad[d][al, j]
         summ = summ / cnt[:, None]
         summd = summd / cnt[:, None]
         sc = np.abs(summ).mean(-1)
@@ -377,12 +394,13 @@ def aligner_optimize(xs: Sequence[np.ndarray], idx: Sequence[np.ndarray], seq_le
             Td = summd[idx[d]]
             S = sc[idx[d]][..., None]
             Sd = scd[idx[d]][..., None]
+            live = alive[d][..., None].astype(np.float32)
             diff = A[d] - T
             diffd = Ad[d] - Td
-            loss1 += float(np.sum(np.abs(diff / S), dtype=np.float64))
-            loss2 += float(np.sum(np.abs(diffd / Sd), dtype=np.float64))
-            gA = np.sign(diff) / S
-            gAd = np.sign(diffd) / Sd * (-(Ad[d] * Ad[d])) * (A[d] >= _f32(1e-3))
+            loss1 += float(np.sum(np.abs(diff / S) * live, dtype=np.float64))
+            loss2 += float(np.sum(np.abs(diffd / Sd) * live, dtype=np.float64))
+            gA = np.sign(diff) / S * live
+            gAd = np.sign(diffd) / Sd * (-(Ad[d] * Ad[d])) * (A[d] >= _f32(1e-3)) * live
             g = (gA + _f32(depth_w) * gAd) * _f32(loss_scale) / denom
             g_s.append((g * xs[d]).sum(axis=(1, 2)).astype(np.float32))
             g_t.append(g.sum(axis=(1, 2)).astype(np.float32))
@@ -421,8 +439,13 @@ def aligner_indices(seq_len: int, gap: int, window: int) -> np.ndarray:
 def aligner_run(snippets: Sequence[np.ndarray], dilations: Sequence[int], factor=10, border=2,
                 **kw):
     """DepthAligner.run (depth_aligner.py:68-120) + merge_scaled_triplets (:231-262).
-    snippets[d]: [n_d, w, 1, H, W].  Returns (merged [N,1,H,W], scales, translations, hist)."""
+    snippets[d]: [n_d, w_d, 1, H, W].  Returns (merged [N,1,H,W], scales, translations, hist).
+    Rows past Σ w_d in the reference's layout raise its IndexError."""
     w0 = snippets[0].shape[1]
+    ws = [s.shape[1] for s in snippets]
+    for i, w in enumerate(ws):
+        if (i + 1) * w > sum(ws):
+            raise IndexError(f"index {(i + 1) * w - 1} is out of bounds for dimension 0 with size {sum(ws)}")
     gaps = [d - 1 for d in dilations]
     seq_len = snippets[0].shape[0] + (w0 - 1) * gaps[0] + (w0 - 1)
     mn = min(float(s.min()) for s in snippets)
@@ -509,18 +532,22 @@ def pipeline_forward(usd, ucfg, vsd, vcfg, scfg, frames: torch.Tensor, init_nois
                      coalign_kwargs=None, max_vae_bs=4, record=None, refine_step=0, refine_snippet_len=3,
                      refine_start_dilation=6):
     """RollingDepthPipeline.forward (rollingdepth_pipeline.py:193-354), stride 1.
-    frames [N,3,H,W] in [-1,1]; init_noise [1,4,h,w] (broadcast to all frames, :282-288)."""
+    frames [N,3,H,W] in [-1,1]; init_noise [1,4,h,w] (broadcast to all frames, :282-288).
+    snippet_len: one length or one per dilation (:215-226)."""
     N = frames.shape[0]
     dil = list(dilations)
+    slens = list(snippet_len) if isinstance(snippet_len, (list, tuple)) else [snippet_len]
+    if len(slens) == 1:
+        slens = slens * len(dil)  # rollingdepth_pipeline.py:220-223
     if cap_dilation:
-        dil = [cap_max_dilation(N, snippet_len, d) for d in dil]
+        dil = [cap_max_dilation(N, sl, d) for d, sl in zip(dil, slens)]
         refine_start_dilation = cap_max_dilation(N, refine_snippet_len, refine_start_dilation)
     rgb_lat = encode_frames(vsd, vcfg, frames, max_vae_bs)
     noise = init_noise.expand(N, *init_noise.shape[1:])
     sched = DDIM(scfg)
     snippets = []
-    for d in dil:
-        ids = snippet_indices(0, 1, N, snippet_len, d, d)
+    for d, sl in zip(dil, slens):
+        ids = snippet_indices(0, 1, N, sl, d, d)
         lat = snippet_denoise(usd, ucfg, sched, rgb_lat, noise, ids, context)
         nd, w = lat.shape[:2]
         dec = decode_depth(vsd, vcfg, lat.reshape(nd * w, *lat.shape[2:]), max_vae_bs)

@@ -53,7 +53,7 @@ class AlignerArgs(C.Structure):
         ("n_dil", i32),
         ("x", vp * 8), ("s", vp * 8), ("t", vp * 8),
         ("n", i32 * 8), ("stride", i32 * 8),
-        ("w", i32), ("seq_len", i32), ("P", i64),
+        ("w", i32 * 8), ("seq_len", i32), ("P", i64),
         ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("lmda2", f32), ("lmda3", f32),
         ("depth_w", f32), ("loss_scale", f32),
         ("iters", i32),
@@ -73,7 +73,7 @@ _SIGS = {
     "rdmi_groupnorm_stats_partials": (i32, [vp, i64, i32, i64, i32, i32, f32, vp, vp]),
     "rdmi_groupnorm_apply": (i32, [vp, vp, i32, i32, i64, i32, i32, vp, vp, vp, i32, vp]),
     "rdmi_conv3x3_to1_gn_workspace": (i64, [i32, i32, i32]),
-    "rdmi_conv3x3_to1_gn": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, f32, vp, vp, vp]),
+    "rdmi_conv3x3_to1_gn": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, f32, vp, i32, vp, vp]),
     "rdmi_layernorm": (i32, [vp, vp, i32, i64, i32, vp, vp, f32, vp]),
     "rdmi_attention_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i64, i64, i64, i64, i64, i64, i64, i64,
                                  f32, i32, vp]),
@@ -100,10 +100,12 @@ _SIGS = {
     "rdmi_aligner_optimize": (i32, [C.POINTER(AlignerArgs), vp]),
     "rdmi_aligner_prepare": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rdmi_aligner_merge": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32),
-                                 C.POINTER(i32), i32, i32, i64, vp, vp, vp]),
+                                 C.POINTER(i32), C.POINTER(i32), i32, i64, vp, vp, vp]),
     "rdmi_aligner_merge_partial": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32),
-                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64, vp, vp, vp]),
-    "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), i32, i32, i32, i64, vp, vp, vp]),
+                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i64,
+                                         vp, vp, vp]),
+    "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64, vp, vp,
+                                        vp]),
 }
 
 RDMI_F16, RDMI_F32, RDMI_U8 = 0, 1, 2

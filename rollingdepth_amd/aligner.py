@@ -14,6 +14,16 @@ import torch
 from . import kernels as K
 
 
+def check_row_layout(lengths: List[int], num_iterations: int) -> None:
+    """The reference scatters dilation i's slots into rows i·w_i .. i·w_i + w_i − 1 of [Σw, N, P]
+    tensors (depth_aligner.py:169-188); rows past Σw raise its IndexError (first closure call)."""
+    rows = sum(lengths)
+    if num_iterations > 0:
+        for i, w in enumerate(lengths):
+            if (i + 1) * w > rows:
+                raise IndexError(f"index {(i + 1) * w - 1} is out of bounds for dimension 0 with size {rows}")
+
+
 class DepthAligner:
     def __init__(self, device: torch.device, factor: int = 10, lmda: float = 1e-1, lmda2: float = 1e-1,
                  lmda3: float = 1e1, lr: float = 1e-3, num_iterations: int = 2000, border: int = 2,
@@ -59,21 +69,24 @@ class DepthAligner:
     def run(self, snippet_ls: List[torch.Tensor], dilations: List[int], merged_f32: bool = False):
         """depth_aligner.py:68-120.  merged_f32=True (the pipeline's internal use): the merge of f16
         snippets runs in f32 arithmetic and is returned in f32, without the reference's f16 roundings
-        of s·x+t and of the merged map (RollingDepthPipeline.merge_f32)."""
+        of s·x+t and of the merged map (RollingDepthPipeline.merge_f32).
+
+        Snippet lengths may differ per dilation (snippet_ls[d] is [n_d, w_d, 1, H, W]): the sequence
+        length comes from the first dilation (:70-76) and the loss uses the reference's row layout
+        (row i·w_i + j for slot j of dilation i, :169-188 — see aligner.hip), including its
+        IndexError when those rows run past Σ w_i."""
         dev = torch.device(self.device)
         snippet_ls = [s.to(dev) for s in snippet_ls]
         lengths = [s.shape[1] for s in snippet_ls]
-        if len(set(lengths)) != 1:
-            raise NotImplementedError("DepthAligner (librdmi): all dilations must share one snippet length")
-        w = lengths[0]
         gaps = [d - 1 for d in dilations]
-        seq_len = self.sequence_length([s.shape[0] for s in snippet_ls], w, dilations)
-        for s, g in zip(snippet_ls, gaps):
+        seq_len = self.sequence_length([s.shape[0] for s in snippet_ls], lengths[0], dilations)
+        for s, g, w in zip(snippet_ls, gaps, lengths):
             expect = seq_len - (w - 1) * (g + 1)
             if s.shape[0] != expect:
-                raise ValueError(f"snippet count {s.shape[0]} != {expect} for dilation {g + 1}")
+                raise ValueError(f"snippet count {s.shape[0]} != {expect} for dilation {g + 1} (length {w})")
+        check_row_layout(lengths, self.num_iterations)
         dtype = snippet_ls[0].dtype
-        flat = [s.reshape(s.shape[0], w, s.shape[-2], s.shape[-1]).contiguous() for s in snippet_ls]
+        flat = [s.reshape(s.shape[0], s.shape[1], s.shape[-2], s.shape[-1]).contiguous() for s in snippet_ls]
         # global min over every snippet (depth_aligner.py:78)
         mins = torch.stack([K.minmax(s) for s in flat]).reshape(-1)
         shift = K.minmax(mins)

@@ -15,12 +15,20 @@
 //                  mul+addcmul, sqrt/bc2_sqrt + eps, addcdiv), loss history row.
 // merge        — merge_scaled_triplets (:231-262): per frame the mean over all covering slots of
 //                s·x+t, rounded through the snippet dtype where the reference computes in it.
+//
+// Snippet lengths may differ per dilation (rollingdepth_pipeline.py:221-226).  The reference then
+// scatters dilation i's slot j into row i·w_i + j of its [Σw, N, P] tensors M / M_depth / B
+// (depth_aligner.py:169-188): rows of different dilations can coincide, and the later dilation's
+// value overwrites the earlier one's at every frame both cover (B stays 1; the overwritten slot
+// gets no gradient).  With one length for all dilations the rows are disjoint and the loops below
+// reduce to the plain per-dilation, per-slot order.
 #pragma clang fp contract(off)
 #include "common.h"
 
 namespace {
 
 constexpr int MAXD = 8;
+constexpr int MAXR = 64;  // rows Σ w_d of the reference's M / M_depth / B tensors
 // Pixel chunks per frame / per snippet: frame_stats and snippet_grad run N·PS and ntot·PS
 // workgroups (one workgroup per frame or snippet alone left most of the 256 CUs idle and each
 // latency-bound), partial sums combined in a fixed chunk order by the consumer (deterministic).
@@ -31,7 +39,8 @@ struct AlP {
   float* s[MAXD];
   float* t[MAXD];
   int n[MAXD], stride[MAXD], off[MAXD];  // off: first global snippet index of dilation d
-  int nd, w, N;
+  int w[MAXD], rb[MAXD];                 // snippet length, first row (d·w_d) of dilation d
+  int nd, R, N;                          // R = Σ w_d rows
   long P;
   float lr, b1, b2, eps, lmda2, lmda3, dw, ls;
   // workspace views
@@ -61,25 +70,52 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
 
 __device__ __forceinline__ long chunk_lo(long P, int c) { return P * c / PS; }
 
+// The (dilation, snippet) whose slot holds row r of frame f in the reference's scatter (the LAST
+// dilation writing that position), or d = -1 when no dilation covers it.
+__device__ __forceinline__ int row_owner(const AlP& p, int r, int f, int& k_out) {
+  for (int d = p.nd - 1; d >= 0; --d) {
+    const int j = r - p.rb[d];
+    if (j < 0 || j >= p.w[d]) continue;
+    const int k = f - j * p.stride[d];
+    if (k < 0 || k >= p.n[d]) continue;
+    k_out = k;
+    return d;
+  }
+  return -1;
+}
+
 // One (frame f, pixel chunk c) work unit of frame_stats; thread 0 returns the chunk's min/max of T.
 __device__ __forceinline__ void frame_stats_body(const AlP& p, int f, int c, float& mn_out, float& mx_out) {
   __shared__ double sh[8];
+  // the slots covering frame f in row order (block-uniform): snippet row pointer, s, t
+  __shared__ const float* ex[MAXR];
+  __shared__ float es[MAXR], et[MAXR];
+  __shared__ int ecnt;
+  if (threadIdx.x == 0) {
+    int cnt = 0;
+    for (int r = 0; r < p.R; ++r) {
+      int k = 0;
+      const int d = row_owner(p, r, f, k);
+      if (d < 0) continue;
+      ex[cnt] = p.x[d] + ((long)k * p.w[d] + (r - p.rb[d])) * p.P;
+      es[cnt] = p.s[d][k];
+      et[cnt] = p.t[d][k];
+      ++cnt;
+    }
+    ecnt = cnt;
+  }
+  __syncthreads();
+  const int cnt = ecnt;
   double sa = 0.0, sd = 0.0;
   float mn = INFINITY, mx = -INFINITY;
   const long p1 = chunk_lo(p.P, c + 1);
   for (long px = chunk_lo(p.P, c) + threadIdx.x; px < p1; px += 256) {
     float sum = 0.f, sumd = 0.f;
-    int cnt = 0;
-    for (int d = 0; d < p.nd; ++d) {
-      for (int j = 0; j < p.w; ++j) {
-        int k = f - j * p.stride[d];
-        if (k < 0 || k >= p.n[d]) continue;
-        float a = addrn(mulrn(p.x[d][((long)k * p.w + j) * p.P + px], p.s[d][k]), p.t[d][k]);
-        float ac = fmaxf(a, 1e-3f);
-        sum = addrn(sum, a);
-        sumd = addrn(sumd, 1.0f / ac);
-        ++cnt;
-      }
+    for (int e = 0; e < cnt; ++e) {
+      float a = addrn(mulrn(ex[e][px], es[e]), et[e]);
+      float ac = fmaxf(a, 1e-3f);
+      sum = addrn(sum, a);
+      sumd = addrn(sumd, 1.0f / ac);
     }
     float T = 0.f, Td = 0.f;
     if (cnt) {
@@ -144,10 +180,12 @@ __device__ __forceinline__ void snippet_grad_body(const AlP& p, int gk, int c, d
   while (d + 1 < p.nd && gk >= p.off[d + 1]) ++d;
   const int k = gk - p.off[d];
   const float s = p.s[d][k], t = p.t[d][k];
-  const float* x = p.x[d] + (long)k * p.w * p.P;
+  const float* x = p.x[d] + (long)k * p.w[d] * p.P;
   double gs = 0.0, gt = 0.0, l1 = 0.0, l2 = 0.0;
-  for (int j = 0; j < p.w; ++j) {
+  for (int j = 0; j < p.w[d]; ++j) {
     const int f = k + j * p.stride[d];
+    int kk = 0;
+    if (row_owner(p, p.rb[d] + j, f, kk) != d) continue;  // overwritten by a later dilation's slot
     float scf, scdf;
     frame_scales(p, f, scf, scdf);
     const float isc = 1.0f / scf, iscd = 1.0f / scdf;
@@ -299,22 +337,27 @@ __global__ __launch_bounds__(256) void adam_step(AlP p, int step, double denom) 
 }
 
 // snippet_grad with Adam fused in (the default loop: two launches per iteration).  The workgroup
-// that finishes the LAST pixel chunk of snippet gk (a per-snippet arrival counter, agent-scope
-// release/acquire) applies Adam to s_gk and t_gk right there: their gradients need nothing else,
-// and every reader of s_gk, t_gk in this launch is one of those chunks.  The loss history is
-// deferred: the iteration's loss partials (hl), pre-update parameters (hst) and, in frame_stats,
-// chunk min/max (hmm) go to per-iteration slots and aligner_history turns them into rows once,
-// after the loop.  Same arithmetic in the same order as snippet_grad + adam_step: bitwise the
+// that finishes the LAST pixel chunk of snippet gk (a per-snippet arrival counter) applies Adam to
+// s_gk and t_gk right there: their gradients need nothing else, and every reader of s_gk, t_gk in
+// this launch is one of those chunks.  The hand-off is NOT a C++ release/acquire: the partials are
+// relaxed agent-scope atomic stores, thread 0 waits for them with s_waitcnt vmcnt(0) (on gfx9 —
+// this library is built for gfx950 only — vmcnt counts stores, and agent-scope atomics bypass the
+// non-coherent caches, so they are visible device-wide once counted), then arrives with a relaxed
+// fetch_add; the last arriver reads the partials as relaxed agent-scope atomic loads.  A true
+// agent-scope release/acquire writes back / invalidates the XCD's whole L2 (1.6x slower loop).
+// The loss history is deferred: the iteration's loss partials (hl), pre-update parameters (hst)
+// and, in frame_stats, chunk min/max (hmm) go to per-iteration slots, and aligner_history turns
+// each block of HBLK iterations into rows.  Same arithmetic in the same order as snippet_grad + adam_step: bitwise the
 // same results (tests/test_aligner_gpu.py::test_aligner_fused_loop_bitwise).
-__global__ __launch_bounds__(256) void snippet_grad_adam(AlP p, int it, double denom, unsigned* cnt, double* hl,
-                                                         float* hst) {
+__global__ __launch_bounds__(256) void snippet_grad_adam(AlP p, int it, long slot, double denom, unsigned* cnt,
+                                                         double* hl, float* hst) {
   const long nps = (long)p.ntot * PS;
   const int gk = blockIdx.x;
-  double* l1o = hl ? hl + (long)(it - 1) * 2 * nps : p.l1;
+  double* l1o = hl ? hl + slot * 2 * nps : p.l1;
   snippet_grad_body<true>(p, gk, blockIdx.y, l1o, l1o + nps);
-  // Hand-off without cache maintenance (an agent-scope fence writes back / invalidates the whole
-  // L2 — 1.6x slower over the loop): the partials were stored as device-coherent atomics by thread 0,
-  // which waits for them to complete before it arrives; the last arriver reads them the same way.
+  // Hand-off without cache maintenance (see above): the partials were stored as agent-scope atomics
+  // by thread 0, which waits for their completion (vmcnt) before it arrives; the last arriver reads
+  // them the same way.
   __shared__ unsigned last;
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -325,7 +368,7 @@ __global__ __launch_bounds__(256) void snippet_grad_adam(AlP p, int it, double d
   if (threadIdx.x < 2) {
     const int i = threadIdx.x ? p.ntot + gk : gk;
     const float pv = adam_param<true>(p, i, it, denom);
-    if (hst) hst[(long)(it - 1) * 2 * p.ntot + i] = pv;
+    if (hst) hst[slot * 2 * p.ntot + i] = pv;
   }
   if (threadIdx.x == 0) cnt[gk] = 0u;  // re-armed for the next iteration (next launch)
 }
@@ -340,14 +383,16 @@ __global__ __launch_bounds__(256) void frame_stats_hist(AlP p, float* hmm) {
   }
 }
 
-// History rows of the fused loop, one workgroup per iteration.
+// History rows of the fused loop for iterations it0 .. it0+gridDim.x-1, one workgroup per iteration;
+// their per-iteration slots are slots 0 .. gridDim.x-1 (the loop writes iteration it into slot
+// (it − 1) mod HBLK and turns every block of HBLK iterations into rows before reusing the slots).
 __global__ __launch_bounds__(256) void aligner_history(AlP p, double denom, const double* hl, const float* hmm,
-                                                       const float* hst) {
-  const int it = blockIdx.x + 1;
+                                                       const float* hst, int it0) {
+  const int slot = blockIdx.x, it = it0 + blockIdx.x;
   const long nps = (long)p.ntot * PS, nfs = (long)p.N * PS;
-  const double* l1 = hl + (long)(it - 1) * 2 * nps;
-  const float* mm = hmm + (long)(it - 1) * nfs * 2;
-  hist_row(p, it, denom, l1, l1 + nps, hst + (long)(it - 1) * 2 * p.ntot, [&](long i, float& lo, float& hi) {
+  const double* l1 = hl + (long)slot * 2 * nps;
+  const float* mm = hmm + (long)slot * nfs * 2;
+  hist_row(p, it, denom, l1, l1 + nps, hst + (long)slot * 2 * p.ntot, [&](long i, float& lo, float& hi) {
     lo = mm[i * 2];
     hi = mm[i * 2 + 1];
   });
@@ -361,9 +406,9 @@ struct MergeP {
   const void* x[MAXD];
   const float* s[MAXD];
   const float* t[MAXD];
-  int n[MAXD], stride[MAXD];
+  int n[MAXD], stride[MAXD], w[MAXD];
   int k0[MAXD], nloc[MAXD];  // rows of x[d] are global snippets k0[d] .. k0[d]+nloc[d]-1
-  int nd, w, xf32;
+  int nd, xf32;
   int sum_only;              // 1: write the per-frame sum (sharded merge), 0: the mean
   int f0;                    // first frame of out (out rows are frames f0 .. f0+gridDim.y-1)
   long HW;
@@ -373,10 +418,10 @@ struct MergeP {
 
 // number of (dilation, slot) pairs covering frame f (the B.sum(0) of depth_aligner.py:190 / the
 // length of the torch.cat of :258)
-__device__ __forceinline__ int cover_count(const int* n, const int* stride, int nd, int w, int f) {
+__device__ __forceinline__ int cover_count(const int* n, const int* stride, int nd, const int* w, int f) {
   int cnt = 0;
   for (int d = 0; d < nd; ++d)
-    for (int j = 0; j < w; ++j) {
+    for (int j = 0; j < w[d]; ++j) {
       const int k = f - j * stride[d];
       cnt += (k >= 0 && k < n[d]) ? 1 : 0;
     }
@@ -390,10 +435,10 @@ __global__ void merge_k(MergeP p) {
     float sum = 0.f;
     int cnt = 0;
     for (int d = 0; d < p.nd; ++d) {
-      for (int j = p.w - 1; j >= 0; --j) {  // boolean-mask order over [n_d, w]: k ascending
+      for (int j = p.w[d] - 1; j >= 0; --j) {  // boolean-mask order over [n_d, w]: k ascending
         int k = f - j * p.stride[d];
         if (k < p.k0[d] || k >= p.k0[d] + p.nloc[d]) continue;
-        long off = ((long)(k - p.k0[d]) * p.w + j) * p.HW + px;
+        long off = ((long)(k - p.k0[d]) * p.w[d] + j) * p.HW + px;
         float a;
         if (p.xf32 == 1) {
           float xs = ((const float*)p.x[d])[off] - sh;
@@ -451,13 +496,19 @@ __global__ void prepare_k(PrepP p) {
   }
 }
 
+// Iterations per block of history slots: the fused loop keeps per-iteration loss partials for at
+// most HBLK iterations, so the workspace does not grow with the iteration count (1500 frames with
+// [1,10,25] at 2000 iterations would otherwise need 1.4 GB).
+constexpr int HBLK = 128;
+
 // Workspace (floats): 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v
 // (2·ntot each), the per-snippet arrival counters (ntot, padded to 8 B); with a history, the
-// fused loop's per-iteration slots: loss partials (2·ntot·PS doubles), chunk min/max (2·N·PS)
-// and pre-update parameters (2·ntot).
+// fused loop's per-iteration slots for min(iters, HBLK) iterations: loss partials (2·ntot·PS
+// doubles), chunk min/max (2·N·PS) and pre-update parameters (2·ntot).
 long ws_floats(int N, long P, int ntot, int iters, bool hist) {
   long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L);
-  if (hist) f += (long)iters * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
+  const long slots = iters < HBLK ? iters : HBLK;
+  if (hist) f += slots * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
   return f + 64;
 }
 
@@ -476,12 +527,11 @@ extern "C" long rdmi_aligner_workspace(const rdmi_aligner_args* a) {
 }
 
 extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
-  RDMI_REQUIRE(a && a->workspace && a->n_dil >= 1 && a->n_dil <= MAXD && a->w >= 1 && a->P > 0 && a->seq_len > 0,
+  RDMI_REQUIRE(a && a->workspace && a->n_dil >= 1 && a->n_dil <= MAXD && a->P > 0 && a->seq_len > 0,
                RDMI_E_ARG, "aligner_optimize: bad args");
   hipStream_t st = (hipStream_t)stream;
   AlP p{};
   p.nd = a->n_dil;
-  p.w = a->w;
   p.N = a->seq_len;
   p.P = a->P;
   int ntot = 0;
@@ -494,6 +544,16 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
     p.stride[d] = a->stride[d];
     p.off[d] = ntot;
     ntot += a->n[d];
+    RDMI_REQUIRE(a->w[d] >= 1, RDMI_E_ARG, "aligner_optimize: snippet length %d of dilation %d", a->w[d], d);
+    p.w[d] = a->w[d];
+    p.R += a->w[d];
+  }
+  RDMI_REQUIRE(p.R <= MAXR, RDMI_E_ARG, "aligner_optimize: %d rows (at most %d)", p.R, MAXR);
+  for (int d = 0; d < p.nd; ++d) {
+    p.rb[d] = d * p.w[d];  // the reference's torch.arange(i * w, (i + 1) * w), depth_aligner.py:182-188
+    RDMI_REQUIRE(a->iters == 0 || p.rb[d] + p.w[d] <= p.R, RDMI_E_ARG,
+                 "aligner_optimize: dilation %d rows %d..%d exceed the %d rows (the reference raises IndexError)", d,
+                 p.rb[d], p.rb[d] + p.w[d] - 1, p.R);
   }
   p.ntot = ntot;
   p.lr = a->lr; p.b1 = a->beta1; p.b2 = a->beta2; p.eps = a->eps;
@@ -511,31 +571,36 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   p.v = fw; fw += 2 * ntot;
   unsigned* cnt = (unsigned*)fw; fw += (ntot + 1) & ~1L;
   p.hist = a->history;
-  int W = 0;
-  for (int d = 0; d < p.nd; ++d) W += p.w;
-  const double denom = (double)W * p.N * (double)p.P;  // numel of the [Σw, N, P] loss tensor
+  const double denom = (double)p.R * p.N * (double)p.P;  // numel of the [Σw, N, P] loss tensor
   hipLaunchKernelGGL(zero_f32, dim3(16), dim3(256), 0, st, p.m, 4L * ntot + ((ntot + 1) & ~1L));  // m, v, cnt
   int rc = rdmi::check_launch("aligner_zero");
   if (rc) return rc;
   if (fused_enabled()) {
     double* hl = nullptr;
     float *hmm = nullptr, *hst = nullptr;
+    const long slots = a->iters < HBLK ? a->iters : HBLK;
     if (p.hist) {
       hl = (double*)fw;
-      hmm = (float*)(hl + (long)a->iters * 2 * nps);
-      hst = hmm + (long)a->iters * 2 * p.N * PS;
+      hmm = (float*)(hl + slots * 2 * nps);
+      hst = hmm + slots * 2 * p.N * PS;
     }
+    int it0 = 1;  // first iteration whose history slots are not yet turned into rows
     for (int it = 1; it <= a->iters; ++it) {
+      const long slot = (it - 1) % HBLK;
       hipLaunchKernelGGL(frame_stats_hist, dim3(p.N, PS), dim3(256), 0, st, p,
-                         hmm ? hmm + (long)(it - 1) * 2 * p.N * PS : nullptr);
-      hipLaunchKernelGGL(snippet_grad_adam, dim3(ntot, PS), dim3(256), 0, st, p, it, denom, cnt, hl, hst);
+                         hmm ? hmm + slot * 2 * p.N * PS : nullptr);
+      hipLaunchKernelGGL(snippet_grad_adam, dim3(ntot, PS), dim3(256), 0, st, p, it, slot, denom, cnt, hl, hst);
       rc = rdmi::check_launch("aligner_iteration");
       if (rc) return rc;
+      if (p.hist && (it - it0 + 1 == HBLK || it == a->iters)) {
+        hipLaunchKernelGGL(aligner_history, dim3(it - it0 + 1), dim3(256), 0, st, p, denom, (const double*)hl,
+                           (const float*)hmm, (const float*)hst, it0);
+        rc = rdmi::check_launch("aligner_history");
+        if (rc) return rc;
+        it0 = it + 1;
+      }
     }
-    if (p.hist && a->iters > 0)
-      hipLaunchKernelGGL(aligner_history, dim3(a->iters), dim3(256), 0, st, p, denom, (const double*)hl,
-                         (const float*)hmm, (const float*)hst);
-    return rdmi::check_launch("aligner_history");
+    return 0;
   }
   for (int it = 1; it <= a->iters; ++it) {
     hipLaunchKernelGGL(frame_stats, dim3(p.N, PS), dim3(256), 0, st, p);
@@ -561,15 +626,15 @@ extern "C" int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int 
 }
 
 static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float* const* s, const float* const* t,
-                        const int* n, const int* stride, const int* k0, const int* nloc, int w, int f0, int nf,
+                        const int* n, const int* stride, const int* k0, const int* nloc, const int* w, int f0, int nf,
                         long HW, const float* shift, float* out, int sum_only, void* stream) {
   RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && out && HW > 0 && nf >= 0 && f0 >= 0, RDMI_E_ARG,
                "aligner_merge: bad args");
   MergeP p{};
   for (int d = 0; d < n_dil; ++d) {
     const int kk = k0 ? k0[d] : 0, nl = nloc ? nloc[d] : n[d];
-    RDMI_REQUIRE(kk >= 0 && nl >= 0 && kk + nl <= n[d] && (nl == 0 || (xf[d] && s[d] && t[d])), RDMI_E_ARG,
-                 "aligner_merge: dilation %d rows %d+%d of %d", d, kk, nl, n[d]);
+    RDMI_REQUIRE(kk >= 0 && nl >= 0 && kk + nl <= n[d] && w[d] >= 1 && (nl == 0 || (xf[d] && s[d] && t[d])),
+                 RDMI_E_ARG, "aligner_merge: dilation %d rows %d+%d of %d, length %d", d, kk, nl, n[d], w[d]);
     p.x[d] = xf[d];
     p.s[d] = s[d];
     p.t[d] = t[d];
@@ -577,8 +642,9 @@ static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float
     p.stride[d] = stride[d];
     p.k0[d] = kk;
     p.nloc[d] = nl;
+    p.w[d] = w[d];
   }
-  p.nd = n_dil; p.w = w; p.xf32 = x_f32; p.HW = HW; p.shift = shift; p.out = out;
+  p.nd = n_dil; p.xf32 = x_f32; p.HW = HW; p.shift = shift; p.out = out;
   p.sum_only = sum_only; p.f0 = f0;
   if (nf == 0) return 0;
   long gx = (HW + 255) / 256;
@@ -588,30 +654,31 @@ static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float
 }
 
 extern "C" int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
-                                  const float* const* t, const int* n, const int* stride, int w, int seq_len, long HW,
+                                  const float* const* t, const int* n, const int* stride, const int* w, int seq_len, long HW,
                                   const float* shift, float* out, void* stream) {
   return merge_launch(n_dil, xf, x_f32, s, t, n, stride, nullptr, nullptr, w, 0, seq_len, HW, shift, out, 0, stream);
 }
 
 extern "C" int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                           const float* const* t, const int* n, const int* stride, const int* k0,
-                                          const int* nloc, int w, int seq_len, long HW, const float* shift,
+                                          const int* nloc, const int* w, int seq_len, long HW, const float* shift,
                                           float* sum_out, void* stream) {
   RDMI_REQUIRE(k0 && nloc, RDMI_E_ARG, "aligner_merge_partial: k0/nloc required");
   return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, 0, seq_len, HW, shift, sum_out, 1, stream);
 }
 
-extern "C" int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, int w, int f0, int nf, long HW,
-                                         const float* sum, float* out, void* stream) {
-  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && sum && out && HW > 0 && f0 >= 0 && nf >= 0, RDMI_E_ARG,
-               "aligner_merge_finish: bad args");
+extern "C" int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf,
+                                         long HW, const float* sum, float* out, void* stream) {
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && sum && out && HW > 0 && f0 >= 0 && nf >= 0,
+               RDMI_E_ARG, "aligner_merge_finish: bad args");
   if (nf == 0) return 0;
   MergeP p{};
   for (int d = 0; d < n_dil; ++d) {
     p.n[d] = n[d];
     p.stride[d] = stride[d];
+    p.w[d] = w[d];
   }
-  p.nd = n_dil; p.w = w; p.HW = HW; p.out = out; p.f0 = f0;
+  p.nd = n_dil; p.HW = HW; p.out = out; p.f0 = f0;
   long gx = (HW + 255) / 256;
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(merge_finish_k, dim3((unsigned)gx, nf), dim3(256), 0, (hipStream_t)stream, p, sum);

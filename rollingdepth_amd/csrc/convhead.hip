@@ -181,7 +181,7 @@ __global__ __launch_bounds__(HT) void head_gather(const float* __restrict__ d, i
   out[q] = (T)s;
 }
 
-template <typename T>
+template <typename T, typename U>
 int head_launch(const void* x, int B, int H, int W, int C, int G, const float* mean_rstd, const float* gamma,
                 const float* beta, int silu, const float* w, float bias, void* y, float* workspace, hipStream_t s) {
   const long HW = (long)H * W, P = (long)B * HW;
@@ -205,7 +205,7 @@ int head_launch(const void* x, int B, int H, int W, int C, int G, const float* m
 #undef RDMI_HEAD
     int rc = rdmi::check_launch("conv3x3_to1_gn taps");
     if (rc) return rc;
-    hipLaunchKernelGGL(head_gather_v<T>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (T*)y);
+    hipLaunchKernelGGL(head_gather_v<U>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (U*)y);
     return rdmi::check_launch("conv3x3_to1_gn gather");
   }
   const size_t lds = (size_t)11 * C * sizeof(float);
@@ -213,7 +213,7 @@ int head_launch(const void* x, int B, int H, int W, int C, int G, const float* m
                      gamma, beta, w, silu, workspace, P);
   int rc = rdmi::check_launch("conv3x3_to1_gn taps");
   if (rc) return rc;
-  hipLaunchKernelGGL(head_gather<T>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (T*)y);
+  hipLaunchKernelGGL(head_gather<U>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (U*)y);
   return rdmi::check_launch("conv3x3_to1_gn gather");
 }
 
@@ -223,12 +223,19 @@ extern "C" long rdmi_conv3x3_to1_gn_workspace(int B, int H, int W) { return 9L *
 
 extern "C" int rdmi_conv3x3_to1_gn(const void* x, int dtype, int B, int H, int W, int C, int G, const float* mean_rstd,
                                    const float* gamma, const float* beta, int silu, const float* w, float bias,
-                                   void* y, float* workspace, void* stream) {
+                                   void* y, int y_dtype, float* workspace, void* stream) {
   RDMI_REQUIRE(x && mean_rstd && gamma && beta && w && y && workspace, RDMI_E_ARG, "conv3x3_to1_gn: null pointer");
   RDMI_REQUIRE(B > 0 && H > 0 && W > 0 && C % 8 == 0 && C > 0 && C <= 1024 && G > 0 && C % G == 0, RDMI_E_ARG,
                "conv3x3_to1_gn: bad sizes B=%d H=%d W=%d C=%d G=%d", B, H, W, C, G);
   RDMI_REQUIRE(((uintptr_t)x & 15) == 0, RDMI_E_ALIGN, "conv3x3_to1_gn: x not 16-byte aligned");
+  RDMI_REQUIRE((dtype == RDMI_F16 || dtype == RDMI_F32) && (y_dtype == RDMI_F16 || y_dtype == RDMI_F32), RDMI_E_ARG,
+               "conv3x3_to1_gn: dtype %d / y_dtype %d", dtype, y_dtype);
+  hipStream_t st = (hipStream_t)stream;
   if (dtype == RDMI_F32)
-    return head_launch<float>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, (hipStream_t)stream);
-  return head_launch<f16>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, (hipStream_t)stream);
+    return y_dtype == RDMI_F32
+               ? head_launch<float, float>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, st)
+               : head_launch<float, f16>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, st);
+  return y_dtype == RDMI_F32
+             ? head_launch<f16, float>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, st)
+             : head_launch<f16, f16>(x, B, H, W, C, G, mean_rstd, gamma, beta, silu, w, bias, y, workspace, st);
 }

@@ -445,24 +445,29 @@ def groupnorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
 
 
 def conv3x3_to1_gn(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: int, eps: float, silu: bool,
-                   w9: torch.Tensor, bias: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   w9: torch.Tensor, bias: float, out: Optional[torch.Tensor] = None,
+                   out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     """GroupNorm(+SiLU) → 3×3 conv (pad 1) to one channel, fused (rdmi.h rdmi_conv3x3_to1_gn).
-    x NHWC f16 [B, H, W, C]; w9 f32 [9, C] (tap = 3·dy + dx); returns [B, H, W, 1] f16."""
+    x NHWC f16/f32 [B, H, W, C]; w9 f32 [9, C] (tap = 3·dy + dx); returns [B, H, W, 1] in out_dtype
+    (default: out's dtype, else x's; f16 or f32)."""
     _need_act(x, "conv3x3_to1_gn.x")
     _need(w9, F32, "conv3x3_to1_gn.w9")
     B, H, W, C_ = x.shape
     if w9.shape != (9, C_):
         raise ValueError(f"conv3x3_to1_gn: w9 {tuple(w9.shape)} != (9, {C_})")
     mr = groupnorm_stats(x, groups, eps)
-    out = torch.empty((B, H, W, 1), dtype=x.dtype, device=x.device) if out is None else out
-    if out.numel() != B * H * W or not out.is_contiguous() or out.dtype != x.dtype:
-        raise ValueError("conv3x3_to1_gn: out must be a contiguous [B, H, W, 1] tensor")
+    od = out_dtype if out_dtype is not None else (out.dtype if out is not None else x.dtype)
+    if od not in (F16, F32):
+        raise ValueError(f"conv3x3_to1_gn: output dtype {od} (f16 or f32)")
+    out = torch.empty((B, H, W, 1), dtype=od, device=x.device) if out is None else out
+    if out.numel() != B * H * W or not out.is_contiguous() or out.dtype != od:
+        raise ValueError("conv3x3_to1_gn: out must be a contiguous [B, H, W, 1] tensor of the output dtype")
     ws = _workspace(lib.rdmi_conv3x3_to1_gn_workspace(B, H, W), x.device)
     with _Timed("conv_head", 2.0 * 9 * C_ * B * H * W, f"head B={B} {H}x{W} {C_}->1",
-                x.element_size() * B * H * W * (C_ + 1)):
+                x.element_size() * B * H * W * C_ + out.element_size() * B * H * W):
         check(lib.rdmi_conv3x3_to1_gn(x.data_ptr(), _dtype_code(x), B, H, W, C_, groups, mr.data_ptr(), gamma.data_ptr(),
                                       beta.data_ptr(), int(silu), w9.data_ptr(), float(bias), out.data_ptr(),
-                                      ws.data_ptr(), _stream()), "rdmi_conv3x3_to1_gn")
+                                      _dtype_code(out), ws.data_ptr(), _stream()), "rdmi_conv3x3_to1_gn")
     return out
 
 
@@ -777,7 +782,7 @@ def aligner_optimize(xs: Sequence[torch.Tensor], scales: Sequence[torch.Tensor],
         a.t[d] = t.data_ptr()
         a.n[d] = x.shape[0]
         a.stride[d] = st
-    a.w = xs[0].shape[1]
+        a.w[d] = x.shape[1]
     a.seq_len = seq_len
     a.P = xs[0].shape[2]
     a.lr, a.beta1, a.beta2, a.eps = lr, betas[0], betas[1], eps
@@ -793,10 +798,11 @@ def aligner_optimize(xs: Sequence[torch.Tensor], scales: Sequence[torch.Tensor],
 
 def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: int, shift: torch.Tensor,
                   f32_arith: bool = False) -> torch.Tensor:
-    """xf[d] [n_d, w, H, W] (f16/f32) → [seq_len, H, W] f32.  f16 snippets are merged in the
+    """xf[d] [n_d, w_d, H, W] (f16/f32) → [seq_len, H, W] f32.  f16 snippets are merged in the
     reference's f16 arithmetic unless f32_arith (rdmi.h rdmi_aligner_merge x_f32 = 2)."""
     nd = len(xf)
-    n_, w, H, W = xf[0].shape
+    H, W = xf[0].shape[-2:]
+    wv = (C.c_int * nd)(*[x.shape[1] for x in xf])
     out = torch.empty((seq_len, H, W), dtype=F32, device=xf[0].device)
     xp = (C.c_void_p * nd)(*[x.data_ptr() for x in xf])
     sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
@@ -804,17 +810,18 @@ def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: i
     nn = (C.c_int * nd)(*[x.shape[0] for x in xf])
     stv = (C.c_int * nd)(*list(strides))
     mode = 1 if xf[0].dtype == F32 else (2 if f32_arith else 0)
-    check(lib.rdmi_aligner_merge(nd, xp, mode, sp, tp, nn, stv, w, seq_len, H * W,
+    check(lib.rdmi_aligner_merge(nd, xp, mode, sp, tp, nn, stv, wv, seq_len, H * W,
                                  shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge")
     return out
 
 
 def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int], n: Sequence[int], scales, trans,
-                          strides, w: int, seq_len: int, HW: int, shift: torch.Tensor, x_f32,
+                          strides, w: Sequence[int], seq_len: int, HW: int, shift: torch.Tensor, x_f32,
                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Sharded merge, rank-local half: xf[d] [nloc_d, w, H, W] = global snippets k0[d] .. of dilation
+    """Sharded merge, rank-local half: xf[d] [nloc_d, w_d, H, W] = global snippets k0[d] .. of dilation
     d (None / 0 rows when the rank owns none) → f32 [seq_len, HW] per-frame sums of s·x+t."""
     nd = len(xf)
+    wv = (C.c_int * nd)(*list(w))
     out = torch.empty((seq_len, HW), dtype=F32, device=shift.device) if out is None else out
     xp = (C.c_void_p * nd)(*[(x.data_ptr() if x is not None and x.shape[0] else None) for x in xf])
     sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
@@ -823,19 +830,22 @@ def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int
     kk = (C.c_int * nd)(*list(k0))
     nl = (C.c_int * nd)(*[(x.shape[0] if x is not None else 0) for x in xf])
     stv = (C.c_int * nd)(*list(strides))
-    check(lib.rdmi_aligner_merge_partial(nd, xp, int(x_f32), sp, tp, nn, stv, kk, nl, w, seq_len, HW,
+    check(lib.rdmi_aligner_merge_partial(nd, xp, int(x_f32), sp, tp, nn, stv, kk, nl, wv, seq_len, HW,
                                          shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge_partial")
     return out
 
 
-def aligner_merge_finish(sums: torch.Tensor, n: Sequence[int], strides: Sequence[int], w: int, f0: int) -> torch.Tensor:
-    """Sharded merge, after the reduce-scatter: f32 [nf, HW] sums of frames f0 .. → per-frame means."""
+def aligner_merge_finish(sums: torch.Tensor, n: Sequence[int], strides: Sequence[int], w: Sequence[int],
+                         f0: int) -> torch.Tensor:
+    """Sharded merge, after the reduce-scatter: f32 [nf, HW] sums of frames f0 .. → per-frame means
+    (w: snippet length per dilation)."""
     nf, HW = sums.shape
     nd = len(n)
     out = torch.empty_like(sums)
     nn = (C.c_int * nd)(*list(n))
     stv = (C.c_int * nd)(*list(strides))
-    check(lib.rdmi_aligner_merge_finish(nd, nn, stv, w, f0, nf, HW, sums.data_ptr(), out.data_ptr(), _stream()),
+    wv = (C.c_int * nd)(*list(w))
+    check(lib.rdmi_aligner_merge_finish(nd, nn, stv, wv, f0, nf, HW, sums.data_ptr(), out.data_ptr(), _stream()),
           "rdmi_aligner_merge_finish")
     return out
 

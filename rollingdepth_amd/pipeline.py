@@ -117,6 +117,12 @@ class RollingDepthPipeline:
         # roundings of the extreme pixels rescale the whole renormalised map — tools/precision_probe.py:
         # 768² depth L1 vs the fp32 reference 1.13e-3 → 7.6e-4).  RDMI_MERGE_F32=0: the fp16 roundings.
         self.merge_f32 = os.environ.get("RDMI_MERGE_F32", "1") == "1"
+        # The decoded depth (the decoder head's output, snippet_ls, the aligner / merge inputs and the
+        # refined depth) is kept in f32 in the f16 pipeline: the f16 rounding of |d| ≈ 1–2 (ulp 1–2e-3)
+        # otherwise reaches the global min/max renormalisation (rollingdepth_pipeline.py:316-318)
+        # directly, where it moves the whole map.  The returned snippet_ls keeps the
+        # reference's dtype (the pipeline's).  RDMI_DEPTH_F32=0: f16 decoded depth.
+        self.depth_f32 = os.environ.get("RDMI_DEPTH_F32", "1") == "1"
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -161,6 +167,11 @@ class RollingDepthPipeline:
     @property
     def dtype(self):
         return self.unet.dtype
+
+    @property
+    def depth_dtype(self):
+        """Storage dtype of decoded depth on the device (f32 unless RDMI_DEPTH_F32=0)."""
+        return F32 if self.depth_f32 else self.dtype
 
     def to(self, *args, **kwargs):
         """DiffusionPipeline.to (pipeline_utils.py:303): weights already live on the device the
@@ -282,7 +293,7 @@ class RollingDepthPipeline:
         return _balanced(n, cap)
 
     def decode_depth(self, z_scaled: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
-        """z_scaled: NHWC [B, h, w, 8] already divided by 0.18215 → out [B, H, W, 1] depth."""
+        """z_scaled: NHWC [B, h, w, 8] already divided by 0.18215 → out [B, H, W, 1] depth (f16 / f32)."""
         for i0, i1 in self._vae_chunks(z_scaled.shape[0], z_scaled.shape[1], z_scaled.shape[2]):
             self.vae.decode_depth(z_scaled[i0:i1], out=out[i0:i1])
         return out
@@ -312,7 +323,7 @@ class RollingDepthPipeline:
                            snippet_subset=None, record: Optional[dict] = None) -> List[torch.Tensor]:
         """rollingdepth_pipeline.py:356-463 with snippets batched per UNet call.
         rgb_latent NHWC [N,h,w,8]; init_noise NHWC [1,h,w,8].  Returns per dilation the decoded
-        snippets [n_d, w, H, W] f16 (device).  `snippet_subset[d]` (optional) restricts the work
+        snippets [n_d, w, H, W] in depth_dtype (device).  `snippet_subset[d]` (optional) restricts the work
         to those snippet indices (multi-GPU sharding); other rows are left uninitialised."""
         self._context()
         N, h, w, _ = rgb_latent.shape
@@ -324,7 +335,7 @@ class RollingDepthPipeline:
             idx = self.get_snippet_indice(0, timesteps, N, slen, dil, dil, stride)
             todo = list(range(len(idx))) if snippet_subset is None else list(snippet_subset[di])
             # row r of the output is snippet todo[r] (all snippets unless a subset is given)
-            buf = torch.empty((len(todo), slen, H, W), dtype=self.dtype, device=self.device)
+            buf = torch.empty((len(todo), slen, H, W), dtype=self.depth_dtype, device=self.device)
             fidx_all = self._device_index([f for s in todo for f in idx[s]]) if todo else None
             for b0, b1 in self._snippet_batches(len(todo), slen, h, w):
                 sel = todo[b0:b1]
@@ -453,21 +464,20 @@ class RollingDepthPipeline:
         return out
 
     def _forward_sharded(self, input_frames, dilations, snippet_lengths, coalign_kwargs, refine_step,
-                         refine_snippet_len, refine_start_dilation, init_noise, record):
+                         refine_snippet_len, refine_start_dilation, init_noise, record, generator=None):
         """forward() over W ranks (shard.sharded_forward), outputs assembled on every rank.  Dilations
         arrive already capped (forward's checks ran); the snippets are all-gathered at full
         resolution only here, to honour the snippet_ls contract (bench.py keeps them distributed)."""
         import torch.distributed as dist
         from .shard import gather_rows_by_dilation, sharded_forward
 
-        if len(set(snippet_lengths)) != 1:
-            raise NotImplementedError("snippet-parallel forward: one snippet length for all dilations")
         world = dist.get_world_size(self._group)
-        so = sharded_forward(self, input_frames, list(dilations), False, snippet_lengths[0], coalign_kwargs,
+        so = sharded_forward(self, input_frames, list(dilations), False, list(snippet_lengths), coalign_kwargs,
                              init_noise=init_noise, group=self._group, refine_step=refine_step,
                              refine_snippet_len=refine_snippet_len, refine_start_dilation=refine_start_dilation,
-                             gather=True, record=record)
-        snips = gather_rows_by_dilation(so.snippet_rows, so.snippet_counts, world, self._group)
+                             gather=True, record=record, generator=generator)
+        snips = gather_rows_by_dilation([r.to(self.dtype) for r in so.snippet_rows], so.snippet_counts, world,
+                                        self._group)
         H, W = so.depth_pred_full.shape[-2:]
         d2h = torch.cuda.Stream(self.device)
         snip_host = [self._to_host_async(s.view(s.shape[0], s.shape[1], 1, H, W), d2h) for s in snips]
@@ -513,7 +523,8 @@ class RollingDepthPipeline:
             import torch.distributed as dist
             if dist.get_world_size(self._group) > 1:
                 return self._forward_sharded(input_frames, dilations, snippet_lengths, coalign_kwargs, refine_step,
-                                             refine_snippet_len, refine_start_dilation, init_noise, record)
+                                             refine_snippet_len, refine_start_dilation, init_noise, record,
+                                             generator)
         # ----------------- encode (H2D boundary :263)
         frames = input_frames[0].to(self.device)
         rgb_latent = self.encode_rgb(frames)
@@ -527,7 +538,8 @@ class RollingDepthPipeline:
         # snippet_ls D2H (the reference returns it on the host) overlaps the aligner's kernels
         H, W = snippets[0].shape[-2:]
         d2h = torch.cuda.Stream(self.device)
-        snip_host = [self._to_host_async(s.view(s.shape[0], s.shape[1], 1, H, W), d2h) for s in snippets]
+        snip_host = [self._to_host_async(s.to(self.dtype).view(s.shape[0], s.shape[1], 1, H, W), d2h)
+                     for s in snippets]
         # ----------------- co-alignment + renormalisation (:306-318)
         aligner = DepthAligner(device=self.device, verbose=verbose, **(coalign_kwargs or {}))
         merged, scales, trans, hist = aligner.run([s.view(s.shape[0], s.shape[1], 1, H, W) for s in snippets],
@@ -545,9 +557,9 @@ class RollingDepthPipeline:
             if record is not None:
                 record["refined_latent"] = new
             z = K.ddim_combine(new[..., :4], new[..., :4], 1.0 / self.depth_latent_scale_factor, 0.0, 1.0, 4, 8)
-            dec = torch.empty((N, H, W, 1), dtype=self.dtype, device=self.device)
+            dec = torch.empty((N, H, W, 1), dtype=self.depth_dtype, device=self.device)
             self.decode_depth(z, dec)
-            depth = dec.view(N, 1, H, W)
+            depth = dec.view(N, 1, H, W).to(self.dtype)
         else:
             depth = coaligned
         # ----------------- outputs (:345-353, D2H boundary; pinned, async, one sync)

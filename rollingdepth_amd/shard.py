@@ -31,7 +31,8 @@ the single-GPU result (tests/test_pipeline_gpu.py); with W = 1 the plan reproduc
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+import math
+from typing import List, Optional, Sequence, Tuple, Union
 
 import torch
 import torch.distributed as dist
@@ -114,19 +115,47 @@ def _reduce_scatter_rows(full: torch.Tensor, world: int, group=None) -> torch.Te
     return out[:hi - lo]
 
 
+def _broadcast(t: torch.Tensor, src: int = 0, group=None):
+    """Broadcast from the group's rank `src` (device tensors staged through the host under gloo)."""
+    root = dist.get_global_rank(group, src) if group is not None and group != dist.group.WORLD else src
+    if _via_host(group, t):
+        h = t.cpu()
+        dist.broadcast(h, root, group=group)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, root, group=group)
+
+
 def gather_rows_by_dilation(local: Sequence[torch.Tensor], counts: Sequence[int], world: int,
                             group=None) -> List[torch.Tensor]:
-    """Every rank's rows (its flat range, per dilation in `local`) all-gathered and split back
-    per dilation: → [n_d, ...] for every d."""
-    ref = next((t for t in local if t is not None), None)
-    flat_local = torch.cat([t for t in local if t is not None and t.shape[0]]) if any(
-        t is not None and t.shape[0] for t in local) else torch.zeros((0, *ref.shape[1:]), dtype=ref.dtype,
-                                                                      device=ref.device)
-    allrows = _all_gather_rows(flat_local, sum(counts), world, group)
-    per_d, o = [], 0
-    for n in counts:
-        per_d.append(allrows[o:o + n])
-        o += n
+    """Every rank's rows (its part of the flat split rank_subsets(counts, world, rank), per dilation
+    in `local`: [m_d, *row_shape_d], row shapes may differ per dilation — snippet lengths per
+    dilation) all-gathered and split back per dilation: → [n_d, *row_shape_d] for every d.
+    One all-gather of each rank's rows flattened into one buffer (padded to the largest rank's)."""
+    shapes = [tuple(t.shape[1:]) for t in local]
+    sizes = [math.prod(sh) for sh in shapes]
+    ref = local[0]
+    plan = [rank_subsets(counts, world, r) for r in range(world)]
+    per_rank = [sum(len(sub[d]) * sizes[d] for d in range(len(counts))) for sub in plan]
+    cap = max(max(per_rank), 1)
+    rank = dist.get_rank(group)
+    for d, t in enumerate(local):
+        if t.shape[0] != len(plan[rank][d]):
+            raise ValueError(f"rank {rank} holds {t.shape[0]} rows of dilation {d}, its plan {len(plan[rank][d])}")
+    flat = torch.zeros(cap, dtype=ref.dtype, device=ref.device)
+    if per_rank[rank]:
+        torch.cat([t.reshape(-1) for t in local if t.numel()], out=flat[:per_rank[rank]])
+    allv = torch.empty(cap * world, dtype=ref.dtype, device=ref.device)
+    _gather_into(allv, flat, group)
+    per_d = [torch.empty((n, *shapes[d]), dtype=ref.dtype, device=ref.device) for d, n in enumerate(counts)]
+    for r in range(world):
+        o = r * cap
+        for d in range(len(counts)):
+            m = len(plan[r][d])
+            if m:
+                k0 = plan[r][d][0]
+                per_d[d][k0:k0 + m] = allv[o:o + m * sizes[d]].view(m, *shapes[d])
+                o += m * sizes[d]
     return per_d
 
 
@@ -148,10 +177,11 @@ class ShardedOutput:
 
 @torch.no_grad()
 def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_dilation: bool = True,
-                    snippet_len: int = 3, coalign_kwargs=None, init_noise: Optional[torch.Tensor] = None, group=None,
-                    num_frames: Optional[int] = None, to_host: bool = False, refine_step: int = 0,
-                    refine_snippet_len: int = 3, refine_start_dilation: int = 6, gather: bool = False,
-                    record: Optional[dict] = None) -> ShardedOutput:
+                    snippet_len: Union[int, Sequence[int]] = 3, coalign_kwargs=None,
+                    init_noise: Optional[torch.Tensor] = None, group=None, num_frames: Optional[int] = None,
+                    to_host: bool = False, refine_step: int = 0, refine_snippet_len: int = 3,
+                    refine_start_dilation: int = 6, gather: bool = False, record: Optional[dict] = None,
+                    generator: Optional[torch.Generator] = None) -> ShardedOutput:
     """Multi-GPU RollingDepthPipeline.forward (every preset: refine_step > 0 included).
 
     `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N` —
@@ -160,18 +190,25 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     every rank copies its own depth / coaligned / input_rgb chunk and its own snippet rows to pinned
     host memory.  `gather=True` also all-gathers the full depth_pred / depth_coaligned on every rank
     (tests, small N).  `dilations` is not mutated (forward() mutates the caller's list; this is the
-    build's own entry point)."""
+    build's own entry point).  `snippet_len`: one length, or one per dilation.  `group` defaults to
+    the world group (refine's all-reduce included).  Without `init_noise` the shared noise is drawn
+    on rank 0 exactly as forward() draws it (from `generator`) and broadcast."""
     from . import kernels as K
-    from .aligner import DepthAligner
+    from .aligner import DepthAligner, check_row_layout
 
+    if group is None:
+        group = dist.group.WORLD
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = pipe.device
     frames = input_frames[0] if input_frames.dim() == 5 else input_frames
     N = frames.shape[0] if num_frames is None else num_frames
     dil = list(dilations)
+    slens = [int(x) for x in snippet_len] if isinstance(snippet_len, (list, tuple)) else [int(snippet_len)] * len(dil)
+    if len(slens) != len(dil):
+        raise ValueError(f"snippet lengths {slens} vs dilations {dil}")
     if cap_dilation:
-        dil = [pipe.cap_max_dilation(N, snippet_len, d) for d in dil]
+        dil = [pipe.cap_max_dilation(N, sl, d) for d, sl in zip(dil, slens)]
         refine_start_dilation = pipe.cap_max_dilation(N, refine_snippet_len, refine_start_dilation)
     if 1 not in dil:
         raise AssertionError("dilations should include 1")
@@ -187,21 +224,25 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     else:
         mine = torch.zeros((0, h, w, pipe.vae.lat_pad), dtype=pipe.dtype, device=dev)
     rgb_latent = _all_gather_rows(mine, N, world, group)
-    if init_noise is None:
-        g = torch.Generator(device=dev).manual_seed(0)
-        init_noise = torch.randn((1, 4, h, w), device=dev, dtype=pipe.dtype, generator=g)
+    if init_noise is None:  # rollingdepth_pipeline.py:282-288, drawn once (rank 0) and broadcast
+        if rank == 0:
+            init_noise = torch.randn((1, 4, h, w), device=dev, dtype=pipe.dtype, generator=generator)
+        else:
+            init_noise = torch.empty((1, 4, h, w), device=dev, dtype=pipe.dtype)
+        _broadcast(init_noise, 0, group)
     noise = pipe._noise_nhwc(init_noise, h, w)
     # 2. my snippets (compact: row r of dilation d is global snippet subsets[d][r])
-    counts = [len(pipe.get_snippet_indice(0, [0], N, snippet_len, d, d, 1)) for d in dil]
+    counts = [len(pipe.get_snippet_indice(0, [0], N, sl, d, d, 1)) for d, sl in zip(dil, slens)]
     subsets = rank_subsets(counts, world, rank)
     k0 = [s[0] if s else 0 for s in subsets]
-    rows = pipe.init_snippet_infer(rgb_latent, noise, dil, [snippet_len] * len(dil), [1] * len(dil), [1] * len(dil),
+    aligner = DepthAligner(device=dev, **(coalign_kwargs or {}))
+    check_row_layout(slens, aligner.num_iterations)
+    rows = pipe.init_snippet_infer(rgb_latent, noise, dil, slens, [1] * len(dil), [1] * len(dil),
                                    snippet_subset=subsets)
     H, W = rows[0].shape[-2:]
     d2h = torch.cuda.Stream(dev) if to_host else None
-    snip_host = [pipe._to_host_async(r, d2h) if r.shape[0] else None for r in rows] if to_host else None
+    snip_host = [pipe._to_host_async(r.to(pipe.dtype), d2h) if r.shape[0] else None for r in rows] if to_host else None
     # 3. co-alignment
-    aligner = DepthAligner(device=dev, **(coalign_kwargs or {}))
     local_mm = [K.minmax(r) for r in rows if r.shape[0]]
     mm = K.minmax(torch.stack(local_mm).reshape(-1)) if local_mm else \
         torch.tensor([float("inf"), float("-inf")], device=dev)
@@ -209,19 +250,19 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     prepared = [aligner.prepare([r], shift)[0] if r.shape[0] else None for r in rows]
     P = ((H - 2 * aligner.border + aligner.factor - 1) // aligner.factor) * \
         ((W - 2 * aligner.border + aligner.factor - 1) // aligner.factor)
-    proto = torch.empty((0, snippet_len, P), dtype=F32, device=dev)
-    xs = gather_rows_by_dilation([p if p is not None else proto for p in prepared], counts, world, group)
+    xs = gather_rows_by_dilation([p if p is not None else torch.empty((0, sl, P), dtype=F32, device=dev)
+                                  for p, sl in zip(prepared, slens)], counts, world, group)
     strides = list(dil)
-    seq_len = aligner.sequence_length(counts, snippet_len, dil)
+    seq_len = aligner.sequence_length(counts, slens[0], dil)
     assert seq_len == N
     scales, trans, hist, ws = aligner.optimize_prepared(xs, strides, N)
+    rows_f32 = rows[0].dtype == F32
     sums = K.aligner_merge_partial([r if r.shape[0] else None for r in rows], k0, counts, scales, trans, strides,
-                                   snippet_len, N, H * W, shift,
-                                   x_f32=1 if pipe.dtype == F32 else (2 if pipe.merge_f32 else 0))
+                                   slens, N, H * W, shift, x_f32=1 if rows_f32 else (2 if pipe.merge_f32 else 0))
     my_sums = _reduce_scatter_rows(sums, world, group)
-    merged = K.aligner_merge_finish(my_sums, counts, strides, snippet_len, f0) if f1 > f0 else my_sums
+    merged = K.aligner_merge_finish(my_sums, counts, strides, slens, f0) if f1 > f0 else my_sums
     # merge_scaled_triplets returns the snippets' dtype (unless the pipeline merges in f32)
-    d = (merged if pipe.merge_f32 else merged.to(pipe.dtype).float()).contiguous()
+    d = (merged if (pipe.merge_f32 or rows_f32) else merged.to(pipe.dtype).float()).contiguous()
     mm_d = K.minmax(d) if d.numel() else torch.tensor([float("inf"), float("-inf")], device=dev)
     gmm = _all_reduce_minmax(mm_d, group)
     if d.numel():
@@ -239,12 +280,12 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
                           group=group)
         if record is not None:
             record["refined_latent"] = new
-        depth = torch.empty((f1 - f0, H, W, 1), dtype=pipe.dtype, device=dev)
+        depth = torch.empty((f1 - f0, H, W, 1), dtype=pipe.depth_dtype, device=dev)
         if f1 > f0:
             z = K.ddim_combine(new[f0:f1, ..., :4], new[f0:f1, ..., :4], 1.0 / pipe.depth_latent_scale_factor, 0.0,
                                1.0, 4, 8)
             pipe.decode_depth(z, depth)
-        depth = depth.view(f1 - f0, 1, H, W)
+        depth = depth.view(f1 - f0, 1, H, W).to(pipe.dtype)
     else:
         depth = coaligned
     if record is not None:

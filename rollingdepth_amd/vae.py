@@ -150,8 +150,8 @@ class VAE:
 
     # ------------------------------------------------------------------ decode
     def decode_depth(self, z: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
-        """z: NHWC f16 [B, h, w, lat_pad] holding latent/0.18215 (zero padded) → depth [B, H, W, 1]
-        = mean over the decoder's RGB outputs."""
+        """z: NHWC [B, h, w, lat_pad] holding latent/0.18215 (zero padded) → depth [B, H, W, 1]
+        = mean over the decoder's RGB outputs, in out's dtype (f16 / f32; default the VAE's)."""
         B, hh, ww, _ = z.shape
         h = torch.zeros((B, hh, ww, self.d_in.cin_pad), dtype=self.dtype, device=z.device)
         self.post_quant(z, out=h)
@@ -166,6 +166,8 @@ class VAE:
                 h = us(h, upsample=True, gn=True)
         # conv_norm_out → SiLU → conv_out (RGB mean folded) as one HBM pass over h (convhead.hip)
         if out is not None and not out.is_contiguous():
+            if out.dtype != self.dtype:
+                raise ValueError("decode_depth: a strided out must have the VAE's dtype")
             h = K.groupnorm(h, self.d_norm.g, self.d_norm.b, self.groups, 1e-6, silu=True)
             return self.d_out(h, out=out)
         return K.conv3x3_to1_gn(h, self.d_norm.g, self.d_norm.b, self.groups, 1e-6, True, self.d_w9, self.d_b,

@@ -14,6 +14,10 @@ Fixtures (all inputs synthesised deterministically, rollingdepth_amd/weights.py)
   attn_processor.safetensors                modified AttnProcessor2_0 (num_view=3 self / cross,
                                             VAE-style 4-D group_norm+residual), fp32
   aligner.safetensors (+ .json)             DepthAligner.run on synthetic snippets, dil [1,4]
+  aligner_mixed.safetensors (+ .json)       DepthAligner.run with snippet lengths [3, 2] (rows of the
+                                            two dilations coincide: the reference's overwrite)
+  tiny_mixed.safetensors (+ .json)          RollingDepthPipeline.forward, tiny, snippet_lengths [3, 2]
+  sd2_768_f32.safetensors (+ .json)         the sd2_768 run stored in f32 (paper-preset precision)
   ddim.json                                 DDIMScheduler timesteps / step / add_noise values
   snippet_indices.json                      get_snippet_indice / cap_max_dilation / aligner indices
 """
@@ -53,7 +57,8 @@ def build_pipe(P, ucfg, vcfg, scfg, seed=0):
     return pipe
 
 
-def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step=0, refine_start=6):
+def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step=0, refine_start=6,
+             snippet_lengths=(3,)):
     rec = {"unet_out": [], "snip_lat": []}
     orig_single = pipe.single_step
     orig_dec = pipe.decode_depth
@@ -80,7 +85,7 @@ def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step
     g = torch.Generator().manual_seed(noise_seed)
     with torch.no_grad():
         out = pipe.forward(
-            input_frames=frames[None], dilations=dil, cap_dilation=cap, snippet_lengths=[3],
+            input_frames=frames[None], dilations=dil, cap_dilation=cap, snippet_lengths=list(snippet_lengths),
             init_infer_steps=[1], strides=[1], coalign_kwargs=coalign, refine_step=refine_step,
             refine_snippet_len=3, refine_start_dilation=refine_start, generator=g, verbose=False,
             max_vae_bs=4, unload_snippet=False)
@@ -119,13 +124,13 @@ def attach_clip(P, pipe):
 
 
 def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, refine_step=0, refine_start=6,
-                     clip=False):
+                     clip=False, snippet_lengths=(3,)):
     pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
     if clip:
         attach_clip(P, pipe)
     h, w = frames.shape[-2] // C.vae_downscale(vcfg), frames.shape[-1] // C.vae_downscale(vcfg)
     noise = torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(1))
-    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign, refine_step, refine_start)
+    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign, refine_step, refine_start, snippet_lengths)
     t = {
         "frames": _c(frames), "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
         "rgb_latent": rec["rgb_latent"], "depth_pred": _c(out.depth_pred),
@@ -140,7 +145,8 @@ def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, 
     save_file(t, os.path.join(HERE, name + ".safetensors"))
     meta = {"dilations_in": list(dilations), "dilations_used": rec["dilations_used"], "cap_dilation": cap,
             "unet": ucfg, "vae": vcfg, "scheduler": C.RD_SCHEDULER, "coalign": coalign or {},
-            "refine_step": refine_step, "refine_start_dilation": refine_start}
+            "refine_step": refine_step, "refine_start_dilation": refine_start,
+            "snippet_lengths": list(snippet_lengths)}
     if clip:  # the context above is the reference's encode_empty_text output
         meta.update(text_encoder=TINY_CLIP, tokenizer_vocab=TINY_VOCAB, text_encoder_seed=0)
     json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
@@ -151,12 +157,15 @@ def _h16(t):
     return t.detach().to(torch.float16).contiguous().clone()
 
 
-def compact_fixture(P, name, ucfg, vcfg, n, res, dilations, cap, depth_stride, refine_step=0, refine_start=6):
+def compact_fixture(P, name, ucfg, vcfg, n, res, dilations, cap, depth_stride, refine_step=0, refine_start=6,
+                    store=None):
     """Large-resolution fixture (768² / 1024²) kept small enough to commit: the frames are NOT
     stored (the GPU test re-synthesises them with weights.synth_frames(n, res, res, seed=0), bitwise
     the same tensor), latents are stored in f16 (the HIP path stores f16), only the first snippet of
     each dilation is stored, and depth maps are stored f16 on a [::s, ::s] pixel lattice plus the
-    full-map mean / mean-|x| (size-independent checksums of the whole map)."""
+    full-map mean / mean-|x| (size-independent checksums of the whole map).  store=_c keeps every
+    stored tensor in f32 (the f32 path's fixture: f16 storage would hide its 1e-6-level error)."""
+    h16 = store or _h16
     pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
     frames = W.synth_frames(n, res, res, seed=0)
     h = w = res // C.vae_downscale(vcfg)
@@ -166,24 +175,25 @@ def compact_fixture(P, name, ucfg, vcfg, n, res, dilations, cap, depth_stride, r
     t = {
         "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
         "frames_checksum": torch.tensor([frames.double().sum().item(), frames.double().abs().sum().item()]),
-        "rgb_latent": _h16(rec["rgb_latent"]),
-        "unet_out_first": _h16(rec["unet_out"][0]), "unet_out_last": _h16(rec["unet_out"][-1]),
-        "depth_pred_sub": _h16(out.depth_pred[..., ::s, ::s]),
-        "depth_coaligned_sub": _h16(out.depth_coaligned[..., ::s, ::s]),
+        "rgb_latent": h16(rec["rgb_latent"]),
+        "unet_out_first": h16(rec["unet_out"][0]), "unet_out_last": h16(rec["unet_out"][-1]),
+        "depth_pred_sub": h16(out.depth_pred[..., ::s, ::s]),
+        "depth_coaligned_sub": h16(out.depth_coaligned[..., ::s, ::s]),
         "depth_pred_stats": torch.tensor([out.depth_pred.double().mean().item(),
                                           out.depth_pred.double().abs().mean().item()]),
     }
     if refine_step > 0:
-        t["refined_latent"] = _h16(rec["snip_lat"][-1][0])
+        t["refined_latent"] = h16(rec["snip_lat"][-1][0])
     for i, sn in enumerate(out.snippet_ls):
-        t[f"snippet_latent_{i}_first"] = _h16(rec["snip_lat"][i][0])
-        t[f"snippet_{i}_first_sub"] = _h16(sn[0, :, 0, ::s, ::s])
+        t[f"snippet_latent_{i}_first"] = h16(rec["snip_lat"][i][0])
+        t[f"snippet_{i}_first_sub"] = h16(sn[0, :, 0, ::s, ::s])
         t[f"snippet_{i}_stats"] = torch.tensor([sn.double().mean().item(), sn.double().abs().mean().item()])
     save_file(t, os.path.join(HERE, name + ".safetensors"))
     meta = {"n_frames": n, "res": res, "frames_seed": 0, "depth_stride": s, "dilations_in": list(dilations),
             "dilations_used": rec["dilations_used"], "cap_dilation": cap, "unet": ucfg, "vae": vcfg,
             "scheduler": C.RD_SCHEDULER, "coalign": {}, "refine_step": refine_step,
-            "refine_start_dilation": refine_start, "n_unet_calls": len(rec["unet_out"])}
+            "refine_start_dilation": refine_start, "n_unet_calls": len(rec["unet_out"]),
+            "storage": "f32" if store is not None else "f16"}
     json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
     print(name, {k: tuple(v.shape) for k, v in t.items()}, flush=True)
 
@@ -259,16 +269,16 @@ def attn_fixture():
     print("attn_processor", len(out))
 
 
-def aligner_fixture(A):
+def aligner_fixture(A, name="aligner", lengths=(3, 3), dil=(1, 4)):
     g = torch.Generator().manual_seed(3)
     N, H, Wd = 20, 64, 64
-    dil = [1, 4]
+    dil = list(dil)
     base = torch.rand((N, 1, H, Wd), generator=g) * 2 - 1
     snips = []
-    for d in dil:
+    for d, w in zip(dil, lengths):
         gap = d
-        n = N - 2 * gap
-        s = torch.stack([torch.stack([base[i + j * gap] for j in range(3)]) for i in range(n)])
+        n = N - (w - 1) * gap
+        s = torch.stack([torch.stack([base[i + j * gap] for j in range(w)]) for i in range(n)])
         sc = 0.5 + torch.rand((n, 1, 1, 1, 1), generator=g)
         sh = 0.3 * torch.randn((n, 1, 1, 1, 1), generator=g)
         snips.append((s * sc + sh + 0.01 * torch.randn(s.shape, generator=g)).float())
@@ -280,10 +290,10 @@ def aligner_fixture(A):
         out[f"scale_{i}"] = _c(a)
         out[f"trans_{i}"] = _c(b)
     out["loss_hist"] = torch.tensor(np.array(hist, dtype=np.float64))
-    save_file(out, os.path.join(HERE, "aligner.safetensors"))
-    json.dump({"dilations": dil, "N": N, "H": H, "W": Wd, "iterations": 2000},
-              open(os.path.join(HERE, "aligner.json"), "w"))
-    print("aligner", merged.shape)
+    save_file(out, os.path.join(HERE, name + ".safetensors"))
+    json.dump({"dilations": dil, "N": N, "H": H, "W": Wd, "iterations": 2000, "snippet_lengths": list(lengths)},
+              open(os.path.join(HERE, name + ".json"), "w"))
+    print(name, merged.shape)
 
 
 def ddim_fixture():
@@ -345,7 +355,8 @@ def main():
     a = ap.parse_args()
     torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", os.cpu_count() or 8)))
     P, A = _refload.load_reference()
-    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "tiny", "refine", "clip", "colorize", "sd2"]
+    todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "aligner_mixed", "tiny",
+                                             "tiny_mixed", "refine", "clip", "colorize", "sd2"]
     if "keys" in todo:
         keys_fixture()
     if "idx" in todo:
@@ -356,6 +367,8 @@ def main():
         attn_fixture()
     if "aligner" in todo:
         aligner_fixture(A)
+    if "aligner_mixed" in todo:  # snippet lengths per dilation; rows 2 of both dilations coincide
+        aligner_fixture(A, "aligner_mixed", (3, 2), (1, 3))
     if "tiny" in todo:
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_pipeline", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True)
@@ -363,6 +376,9 @@ def main():
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_refine", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, refine_step=2,
                          refine_start=6)
+    if "tiny_mixed" in todo:  # snippet_lengths [3, 2] (rollingdepth_pipeline.py:221-226)
+        frames = W.synth_frames(9, 32, 32, seed=0)
+        pipeline_fixture(P, "tiny_mixed", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, snippet_lengths=(3, 2))
     if "colorize" in todo:
         colorize_fixture()
     if "clip" in todo:  # tiny pipeline whose empty-text context comes from the reference's CLIP path
@@ -374,6 +390,8 @@ def main():
     # large-resolution fixtures (opt-in: --only; tens of CPU-minutes each)
     if "sd2_768" in todo:  # fast preset arithmetic on one 3-frame 768² snippet (SURVEY §8c fixture 3)
         compact_fixture(P, "sd2_768", C.SD2_UNET, C.SD2_VAE, 3, 768, [1], False, 2)
+    if "sd2_768_f32" in todo:  # the same run, stored f32: pins the f32 (paper preset) path at 768²
+        compact_fixture(P, "sd2_768_f32", C.SD2_UNET, C.SD2_VAE, 3, 768, [1], False, 2, store=_c)
     if "sd2_1024" in todo:  # fast1024 preset arithmetic on one 3-frame 1024² snippet
         compact_fixture(P, "sd2_1024", C.SD2_UNET, C.SD2_VAE, 3, 1024, [1], False, 2)
     if "full1024" in todo:  # full preset: 1024², [1,10,25] capped as the reference caps, refine 10

@@ -10,26 +10,29 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _synth(N=14, dil=(1, 3), H=40, W=44, seed=0, dtype=np.float32):
+def _synth(N=14, dil=(1, 3), H=40, W=44, seed=0, dtype=np.float32, lengths=None):
     rng = np.random.default_rng(seed)
     base = rng.uniform(-1, 1, (N, 1, H, W)).astype(np.float32)
     out = []
-    for d in dil:
-        n = N - 2 * d
-        s = np.stack([np.stack([base[i + j * d] for j in range(3)]) for i in range(n)])
+    for d, w in zip(dil, lengths or [3] * len(dil)):
+        n = N - (w - 1) * d
+        s = np.stack([np.stack([base[i + j * d] for j in range(w)]) for i in range(n)])
         sc = 0.5 + rng.uniform(0, 1, (n, 1, 1, 1, 1))
         sh = 0.3 * rng.standard_normal((n, 1, 1, 1, 1))
         out.append((s * sc + sh + 0.01 * rng.standard_normal(s.shape)).astype(dtype))
     return out, list(dil)
 
 
-@pytest.mark.parametrize("iters", [1, 50, 150])
-def test_aligner_optimize_matches_oracle(iters):
+@pytest.mark.parametrize("iters,lengths", [(1, None), (50, None), (150, None), (1, (3, 2)), (50, (3, 2)),
+                                           (50, (4, 2, 2))])
+def test_aligner_optimize_matches_oracle(iters, lengths):
     """Before Adam reaches its oscillating L1 regime (~200-300 it) the trajectories agree to f32
-    rounding: parameters to 2e-5·(iters/50), loss history to 1e-5 relative."""
+    rounding: parameters to 2e-5·(iters/50), loss history to 1e-5 relative.  lengths: snippet
+    lengths per dilation — [3, 2] and [4, 2, 2] put slots of different dilations on the same row
+    of the reference's [Σw, N, P] tensors (the later dilation overwrites, depth_aligner.py:179-188)."""
     from rollingdepth_amd.aligner import DepthAligner
 
-    snips, dil = _synth()
+    snips, dil = _synth(dil=(1, 3, 2)[:len(lengths)] if lengths else (1, 3), lengths=lengths)
     ref_m, ref_s, ref_t, ref_h = O.aligner_run(snips, dil, iters=iters)
     al = DepthAligner(device=torch.device(DEV), num_iterations=iters)
     m, s, t, h = al.run([torch.from_numpy(x).to(DEV) for x in snips], list(dil))
@@ -40,17 +43,19 @@ def test_aligner_optimize_matches_oracle(iters):
     assert np.abs(m.cpu().numpy() - ref_m).max() < 1e-4
 
 
-def test_aligner_2000_iterations_vs_reference_golden():
-    """Full 2000-iteration run on the reference's own aligner fixture (DepthAligner.run output),
-    with the tolerances of tests/test_oracle_golden.py::test_aligner_oracle_vs_reference."""
+@pytest.mark.parametrize("name", ["aligner", "aligner_mixed"])
+def test_aligner_2000_iterations_vs_reference_golden(name):
+    """Full 2000-iteration run on the reference's own aligner fixtures (DepthAligner.run output; the
+    mixed one with snippet lengths [3, 2]), with the tolerances of
+    tests/test_oracle_golden.py::test_aligner_oracle_vs_reference."""
     import json
     import os
     from safetensors.torch import load_file
     from rollingdepth_amd.aligner import DepthAligner
 
     g = os.path.join(os.path.dirname(__file__), "golden")
-    t = load_file(os.path.join(g, "aligner.safetensors"))
-    dil = json.load(open(os.path.join(g, "aligner.json")))["dilations"]
+    t = load_file(os.path.join(g, name + ".safetensors"))
+    dil = json.load(open(os.path.join(g, name + ".json")))["dilations"]
     al = DepthAligner(device=torch.device(DEV), num_iterations=2000)
     m, s, tr, h = al.run([t[f"snippet_{i}"].to(DEV) for i in range(len(dil))], list(dil))
     ref_h = t["loss_hist"].numpy()
@@ -87,17 +92,21 @@ def test_aligner_merge_f16_rounding():
     assert np.abs(got - ref[:, 0].astype(np.float32)).max() <= 2e-3
 
 
-@pytest.mark.parametrize("case", ["small", "metric"])
+@pytest.mark.parametrize("case", ["small", "mixed", "metric"])
 def test_aligner_fused_loop_bitwise(case, monkeypatch):
     """The two-launch iteration (aligner.hip snippet_grad_adam: per-snippet last-chunk Adam, deferred
-    loss history) gives bitwise the scales, translations, loss history and merged depth of the
-    three-kernel loop (RDMI_ALIGNER_FUSED=0).  'metric': the fast preset's aligner shape
-    (N = 100 frames, dilations [1, 25], P = 5 929 subsampled pixels of a 768² frame), 300 iterations."""
+    loss history, turned into rows per block of 128 iterations) gives bitwise the scales,
+    translations, loss history and merged depth of the three-kernel loop (RDMI_ALIGNER_FUSED=0).
+    'metric': the fast preset's aligner shape (N = 100 frames, dilations [1, 25], P = 5 929
+    subsampled pixels of a 768² frame), 300 iterations (three history blocks)."""
     from rollingdepth_amd.aligner import DepthAligner
 
     if case == "small":
         snips, dil = _synth()
         iters = 120
+    elif case == "mixed":
+        snips, dil = _synth(lengths=(3, 2))
+        iters = 130
     else:
         snips, dil = _synth(N=100, dil=(1, 25), H=774, W=774)  # (774 − 4) / 10 → 77² = 5 929 px
         iters = 300
@@ -114,3 +123,14 @@ def test_aligner_fused_loop_bitwise(case, monkeypatch):
     for d in range(len(dil)):
         assert torch.equal(a[1][d], b[1][d]) and torch.equal(a[2][d], b[2][d])
     assert a[3] == b[3]
+
+
+def test_aligner_row_overflow_raises_index_error():
+    """Snippet lengths [2, 3]: the reference's rows 3..5 of a 5-row tensor raise IndexError
+    (depth_aligner.py:182) — raised here before any launch, and the C-ABI rejects the layout too."""
+    from rollingdepth_amd.aligner import DepthAligner
+
+    snips, dil = _synth(lengths=(2, 3))
+    al = DepthAligner(device=torch.device(DEV), num_iterations=5)
+    with pytest.raises(IndexError):
+        al.run([torch.from_numpy(x).to(DEV) for x in snips], list(dil))

@@ -214,13 +214,15 @@ def test_video_target_size_and_missing_pyav():
 def test_aligner_workspace_sizes_history_slots():
     """rdmi_aligner_workspace (host-only, no GPU): the fused aligner loop keeps per-iteration loss
     partials (2·ntot·PS doubles), chunk min/max (2·N·PS floats) and pre-update parameters (2·ntot)
-    when a history is requested, and nothing per iteration without one (aligner.hip ws_floats)."""
+    for one block of at most 128 iterations when a history is requested (aligner.hip HBLK: the
+    workspace does not grow with the iteration count), and nothing per iteration without one."""
     import ctypes as C
 
     from rollingdepth_amd import _native
 
     a = _native.AlignerArgs()
-    a.n_dil, a.w, a.seq_len, a.P = 2, 3, 100, 5929
+    a.n_dil, a.seq_len, a.P = 2, 100, 5929
+    a.w[0], a.w[1] = 3, 3
     a.n[0], a.n[1] = 98, 48
     ntot, PS = 146, 8
     a.iters = 2000
@@ -229,6 +231,9 @@ def test_aligner_workspace_sizes_history_slots():
     assert base >= 8 * ntot * PS + 8 * 100 * PS + 2 * 100 * 5929 + 4 * ntot + ntot
     a.history = 1  # any non-null pointer: the size depends only on its presence
     with_hist = _native.lib.rdmi_aligner_workspace(C.byref(a))
-    assert with_hist - base >= 2000 * (4 * ntot * PS + 2 * 100 * PS + 2 * ntot)
+    per_it = 4 * ntot * PS + 2 * 100 * PS + 2 * ntot
+    assert 128 * per_it <= with_hist - base <= 128 * per_it + 64
+    a.iters = 128
+    assert _native.lib.rdmi_aligner_workspace(C.byref(a)) == with_hist
     a.iters = 10
     assert _native.lib.rdmi_aligner_workspace(C.byref(a)) < with_hist

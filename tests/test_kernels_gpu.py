@@ -355,6 +355,11 @@ def test_conv3x3_to1_gn(B, H, W, C, silu):
     ref = F.conv2d(n, w, torch.tensor([b], device=DEV), padding=1).permute(0, 2, 3, 1)
     assert y.shape == (B, H, W, 1)
     assert (y.float() - ref).abs().max().item() < 5e-3
+    # f32 output (the f16 pipeline's decoded depth, rdmi_conv3x3_to1_gn y_dtype): the same f32 sums,
+    # unrounded — the f16 output is exactly its rounding
+    y32 = K_.conv3x3_to1_gn(x, gm, bt, 32, 1e-6, silu, w9, b, out_dtype=torch.float32)
+    assert y32.dtype == torch.float32 and torch.equal(y32.half(), y)
+    assert (y32 - ref).abs().max().item() < 1e-4
 
 
 @pytest.mark.parametrize("C", [320, 640, 1280])

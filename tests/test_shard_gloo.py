@@ -31,12 +31,13 @@ def _snippet(d, k, shape):
 
 def _merge_partial_cpu(rows, k0, n, strides, scales, trans, w, N, HW):
     """CPU restatement of rdmi_aligner_merge_partial (f32 snippets): per frame the sum over this
-    rank's (dilation, local snippet, slot) of s·x + t, slots in the reference's k-ascending order."""
+    rank's (dilation, local snippet, slot) of s·x + t, slots in the reference's k-ascending order
+    (w: snippet length per dilation)."""
     out = torch.zeros((N, HW), dtype=torch.float32)
     for f in range(N):
         acc = torch.zeros(HW, dtype=torch.float32)
         for d, r in enumerate(rows):
-            for j in range(w - 1, -1, -1):
+            for j in range(w[d] - 1, -1, -1):
                 k = f - j * strides[d]
                 if k < k0[d] or k >= k0[d] + r.shape[0]:
                     continue
@@ -46,15 +47,15 @@ def _merge_partial_cpu(rows, k0, n, strides, scales, trans, w, N, HW):
 
 
 def _cover(n, strides, w, f):
-    return sum(1 for d in range(len(n)) for j in range(w) if 0 <= f - j * strides[d] < n[d])
+    return sum(1 for d in range(len(n)) for j in range(w[d]) if 0 <= f - j * strides[d] < n[d])
 
 
 def _worker(rank, world, port, res):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import rd_oracle as O
-    from rollingdepth_amd.shard import (_all_gather_rows, _all_reduce_minmax, _reduce_scatter_rows, chunk_bounds,
-                                        gather_rows_by_dilation, rank_subsets)
+    from rollingdepth_amd.shard import (_all_gather_rows, _all_reduce_minmax, _broadcast, _reduce_scatter_rows,
+                                        chunk_bounds, gather_rows_by_dilation, rank_subsets)
 
     ok = True
     # --- flat split + all-gather of per-snippet rows (the aligner inputs) -----------------------
@@ -67,6 +68,16 @@ def _worker(rank, world, port, res):
     ok &= all(torch.equal(per_d[d][k], _snippet(d, k, shape)) for d, n in enumerate(counts) for k in range(n))
     # every rank's subset is contiguous within a dilation (compact rows = global k0 ..)
     ok &= all(s == list(range(s[0], s[0] + len(s))) for s in sub if s)
+    # rows of different shapes per dilation (snippet lengths [3, 2]) through the same all-gather
+    shapes = [(3, 2, 5), (2, 2, 5)]
+    local = [torch.stack([_snippet(d, k, shapes[d]) for k in sub[d]]) if sub[d] else torch.zeros((0, *shapes[d]))
+             for d in range(len(counts))]
+    per_d = gather_rows_by_dilation(local, counts, world)
+    ok &= all(torch.equal(per_d[d][k], _snippet(d, k, shapes[d])) for d, n in enumerate(counts) for k in range(n))
+    # the shared init noise drawn on rank 0 and broadcast (sharded_forward without init_noise)
+    nz = torch.randn(1, 4, 3, 3, generator=torch.Generator().manual_seed(5)) if rank == 0 else torch.zeros(1, 4, 3, 3)
+    _broadcast(nz, 0)
+    ok &= torch.equal(nz, torch.randn(1, 4, 3, 3, generator=torch.Generator().manual_seed(5)))
     # --- frame-chunk latents all-gather ------------------------------------------------------------
     N = 11
     lo, hi = chunk_bounds(N, world)[rank]
@@ -76,10 +87,11 @@ def _worker(rank, world, port, res):
     mm = _all_reduce_minmax(torch.tensor([float(rank) - 5.0, 10.0 * rank]))
     ok &= mm.tolist() == [-5.0, 10.0 * (world - 1)]
     # --- merge: rank-local sums, reduce-scatter by frame, ÷ cover count == merge_scaled_triplets -----
-    N, w, H, W = 14, 3, 4, 5
+    N, H, W = 14, 4, 5
+    w = [3, 2]  # snippet lengths per dilation
     dil = [1, 4]
     g = torch.Generator().manual_seed(11)
-    full = [torch.rand((N - (w - 1) * d, w, H, W), generator=g) for d in dil]
+    full = [torch.rand((N - (wd - 1) * d, wd, H, W), generator=g) for d, wd in zip(dil, w)]
     n = [x.shape[0] for x in full]
     sc = [0.5 + torch.rand(m, generator=g) for m in n]
     tr = [0.1 * torch.randn(m, generator=g) for m in n]
@@ -91,7 +103,7 @@ def _worker(rank, world, port, res):
     f0, f1 = chunk_bounds(N, world)[rank]
     merged_mine = torch.stack([mine[i] / _cover(n, dil, w, f0 + i) for i in range(f1 - f0)]) if f1 > f0 else mine
     merged = _all_gather_rows(merged_mine, N, world)
-    idx = [O.aligner_indices(N, d - 1, w) for d in dil]
+    idx = [O.aligner_indices(N, d - 1, wd) for d, wd in zip(dil, w)]
     ref = O.aligner_merge([x.numpy()[:, :, None] for x in full], idx, [s.numpy() for s in sc],
                           [t.numpy() for t in tr], N)
     err = np.abs(merged.numpy() - ref.reshape(N, H * W)).max()

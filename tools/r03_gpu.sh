@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-3 GPU session helper: each step under its own time limit; a fault / abort / segfault / time
+# limit (124 / 134 / 137 / 139) ends the script, plain test failures (1) do not.
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r03}
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+if [ -n "${TESTS:-}" ]; then
+  timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest ${TESTS} -m gpu --maxfail=${MAXFAIL:-10} -v -s \
+    --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
+  rc=$?; echo "tests exit $rc"; if fatal $rc; then exit $rc; fi
+fi
+if [ "${SENS:-0}" = "1" ]; then
+  timeout -k 10 300 python -u tools/depth_sensitivity.py > gpurun_out/${TAG}_depth_sens.log 2>&1
+  rc=$?; echo "sens exit $rc"; if fatal $rc; then exit $rc; fi
+  RDMI_DEPTH_F32=0 timeout -k 10 300 python -u tools/depth_sensitivity.py > gpurun_out/${TAG}_depth_sens_f16.log 2>&1
+  rc=$?; echo "sens f16 exit $rc"; if fatal $rc; then exit $rc; fi
+fi
+if [ -n "${BENCH_ARGS:-}" ]; then
+  timeout -k 10 ${BENCH_TIMEOUT:-400} python -u bench.py ${BENCH_ARGS} > gpurun_out/${TAG}_bench.log 2>&1
+  rc=$?; echo "bench exit $rc"; if fatal $rc; then exit $rc; fi
+fi
+exit 0
