@@ -168,12 +168,13 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
 }
 
 // Streaming apply: each thread owns one 8-channel column (its 16 scale/shift values stay in
-// registers) and walks rows; no per-element division, 16-B loads/stores.
-template <typename T>
+// registers) and walks rows; no per-element division, 16-B loads/stores.  SILU is a template
+// argument (dispatched once per launch): as a runtime flag hipcc if-converts it, computing and
+// discarding a SiLU per element of every non-SiLU apply.
+template <typename T, bool SILU>
 __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x, T* __restrict__ y, long HW, int C,
                                                 int G, int rows_per_block, const float* __restrict__ mr,
-                                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                int silu) {
+                                                const float* __restrict__ gamma, const float* __restrict__ beta) {
   const int CV = C >> 3;
   const int cpg = C / G;
   const int b = blockIdx.y;
@@ -210,7 +211,7 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x, T* __re
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float f = fmaf(in[e], sc[e], sh[e]);
-        if (silu) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
+        if constexpr (SILU) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
         out[e] = f;
       }
       st8(yb + r * C + cv * 8, out);
@@ -343,12 +344,22 @@ extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, lo
   if (rpb < RL) rpb = RL;
   rpb = (rpb + RL - 1) / RL * RL;
   dim3 g((unsigned)((HW + rpb - 1) / rpb), B);
-  if (dtype == RDMI_F32)
-    hipLaunchKernelGGL(gn_apply<float>, g, dim3(T), 0, (hipStream_t)stream, (const float*)x, (float*)y, HW, C, G,
-                       (int)rpb, mean_rstd, gamma, beta, silu);
-  else
-    hipLaunchKernelGGL(gn_apply<f16>, g, dim3(T), 0, (hipStream_t)stream, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
-                       mean_rstd, gamma, beta, silu);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RDMI_F32) {
+    if (silu)
+      hipLaunchKernelGGL((gn_apply<float, true>), g, dim3(T), 0, st, (const float*)x, (float*)y, HW, C, G, (int)rpb,
+                         mean_rstd, gamma, beta);
+    else
+      hipLaunchKernelGGL((gn_apply<float, false>), g, dim3(T), 0, st, (const float*)x, (float*)y, HW, C, G, (int)rpb,
+                         mean_rstd, gamma, beta);
+  } else {
+    if (silu)
+      hipLaunchKernelGGL((gn_apply<f16, true>), g, dim3(T), 0, st, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
+                         mean_rstd, gamma, beta);
+    else
+      hipLaunchKernelGGL((gn_apply<f16, false>), g, dim3(T), 0, st, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
+                         mean_rstd, gamma, beta);
+  }
   return rdmi::check_launch("groupnorm_apply");
 }
 

@@ -93,6 +93,20 @@ def _resolve(d: torch.device) -> torch.device:
     return d
 
 
+_PROGRESS = os.environ.get("RDMI_PROGRESS") == "1"
+
+
+def _progress(msg: str) -> None:
+    """RDMI_PROGRESS=1: wait for the device and print a progress line (long runs — e.g. the paper
+    preset's 500 frames — must show life to a supervisor; off by default: it synchronises)."""
+    if _PROGRESS:
+        import sys
+        import time
+
+        torch.cuda.synchronize()
+        print(f"[rdmi progress {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _contiguous_range(total: int, world: int, rank: int) -> Tuple[int, int]:
     """Rank's share of `total` equal-cost units: W contiguous ranges of ceil(total/W)."""
     c = (total + world - 1) // world
@@ -362,6 +376,7 @@ class RollingDepthPipeline:
                         x = x2
                         depth_view = x[..., 4:8]
                 self.decode_depth(zin, buf[b0:b1].view(len(sel) * slen, H, W, 1))
+                _progress(f"dilation {dil}: snippets {b1}/{len(todo)} decoded")
             outs.append(buf)
         return outs
 
@@ -407,6 +422,7 @@ class RollingDepthPipeline:
                 pred = self.unet.forward(x, int(t), num_view=snippet_len)
                 self.scheduler.step_(pred, int(t), x[..., 4:8], 1.0, channels=4,
                                      out=preds[b0:b0 + len(sel)].view(len(sel) * snippet_len, h, w, 8))
+            _progress(f"refine step {i_step + 1}/{len(ts)}: {len(mine)} snippets")
             if world == 1:
                 new = K.snippet_average(preds, stride, N)
             else:
@@ -547,6 +563,7 @@ class RollingDepthPipeline:
         d = merged.float().contiguous()
         K.renormalize_(d, K.minmax(d))
         coaligned = d.to(self.dtype)
+        _progress("co-alignment done")
         if record is not None:
             record.update(rgb_latent=rgb_latent, scales=scales, translations=trans, loss_history=hist,
                           dilations=list(dilations))

@@ -37,6 +37,27 @@ __global__ __launch_bounds__(256) void probe(float* out, long long* cyc, int ite
       asm volatile(REP16("v_add_f32 %0, %0, %4\n v_add_f32 %1, %1, %5\n v_add_f32 %2, %2, %6\n"
                          "v_add_f32 %3, %3, %7\n")
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a4), "v"(a5), "v"(a6), "v"(a7));
+    } else if (OP == 7) {  // v_pk_fma_f16 (two f16 FMAs per lane: a polynomial exp2 would be built of these)
+      asm volatile(REP16("v_pk_fma_f16 %0, %0, %4, %5\n v_pk_fma_f16 %1, %1, %5, %6\n v_pk_fma_f16 %2, %2, %6, %7\n"
+                         "v_pk_fma_f16 %3, %3, %7, %4\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a4), "v"(a5), "v"(a6), "v"(a7));
+    } else if (OP == 8) {  // v_fma_f32
+      asm volatile(REP16("v_fma_f32 %0, %0, %4, %5\n v_fma_f32 %1, %1, %5, %6\n v_fma_f32 %2, %2, %6, %7\n"
+                         "v_fma_f32 %3, %3, %7, %4\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a4), "v"(a5), "v"(a6), "v"(a7));
+    } else if (OP == 9) {  // v_exp_f32 / v_add_f32 alternating on independent registers: do they overlap?
+      asm volatile(REP16("v_exp_f32 %0, %0\n v_add_f32 %1, %1, %4\n v_exp_f32 %2, %2\n v_add_f32 %3, %3, %5\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a4), "v"(a5));
+    } else if (OP == 10) {  // v_pk_fma_f32 (packed f32 pairs: 64-bit register pairs)
+      double d0 = a0, d1 = a1, d2 = a2, d3 = a3, e0 = a4, e1 = a5;
+      asm volatile(REP16("v_pk_fma_f32 %0, %0, %4, %5\n v_pk_fma_f32 %1, %1, %5, %4\n v_pk_fma_f32 %2, %2, %4, %5\n"
+                         "v_pk_fma_f32 %3, %3, %5, %4\n")
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(e0), "v"(e1));
+      a0 = (float)(d0 + d1);
+      a1 = (float)(d2 + d3);
+    } else if (OP == 11) {  // v_exp_f32 / v_pk_fma_f16 alternating on independent registers
+      asm volatile(REP16("v_exp_f32 %0, %0\n v_pk_fma_f16 %1, %1, %4, %5\n v_exp_f32 %2, %2\n v_pk_fma_f16 %3, %3, %5, %4\n")
+                   : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : "v"(a4), "v"(a5));
     } else if (OP == 6) {  // v_exp_f16 lo + SDWA hi pairs (the packed-P form)
       asm volatile(REP16("v_exp_f16 %0, %4\n v_exp_f16_sdwa %0, %4 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n"
                          "v_exp_f16 %1, %5\n v_exp_f16_sdwa %1, %5 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n")
@@ -76,5 +97,10 @@ int main() {
   run<3>("v_cvt_pk_f16_f32", out, cyc, blocks);
   run<4>("v_pk_add_f16", out, cyc, blocks);
   run<5>("v_add_f32", out, cyc, blocks);
+  run<8>("v_fma_f32", out, cyc, blocks);
+  run<7>("v_pk_fma_f16", out, cyc, blocks);
+  run<10>("v_pk_fma_f32", out, cyc, blocks);
+  run<9>("v_exp_f32 + v_add_f32 alt", out, cyc, blocks);
+  run<11>("v_exp_f32 + v_pk_fma_f16 alt", out, cyc, blocks);
   return 0;
 }

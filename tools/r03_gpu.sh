@@ -6,6 +6,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r03}
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+if [ "${ISA:-0}" = "1" ]; then
+  timeout -k 10 120 ./tools/isa_rate > gpurun_out/${TAG}_isa_rate.log 2>&1
+  rc=$?; echo "isa_rate exit $rc"; if fatal $rc; then exit $rc; fi
+fi
 if [ -n "${TESTS:-}" ]; then
   timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest ${TESTS} -m gpu --maxfail=${MAXFAIL:-10} -v -s \
     --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
