@@ -11,8 +11,8 @@ if [ "${ISA:-0}" = "1" ]; then
   rc=$?; echo "isa_rate exit $rc"; if fatal $rc; then exit $rc; fi
 fi
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest ${TESTS} -m gpu --maxfail=${MAXFAIL:-10} -v -s \
-    --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest ${TESTS} -m gpu ${TESTK:+-k "$TESTK"} \
+    --maxfail=${MAXFAIL:-10} -v -s --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
   rc=$?; echo "tests exit $rc"; if fatal $rc; then exit $rc; fi
 fi
 if [ "${SENS:-0}" = "1" ]; then
@@ -24,5 +24,18 @@ fi
 if [ -n "${BENCH_ARGS:-}" ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-400} python -u bench.py ${BENCH_ARGS} > gpurun_out/${TAG}_bench.log 2>&1
   rc=$?; echo "bench exit $rc"; if fatal $rc; then exit $rc; fi
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  OUT=gpurun_out/${TAG}_pmc PRESET=${PMC_PRESET:-fast} bash tools/pmc_bench.sh > gpurun_out/${TAG}_pmc.log 2>&1
+  rc=$?; echo "pmc exit $rc"; if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+if [ "${PROF:-0}" = "1" ]; then
+  rm -rf gpurun_out/${TAG}_prof
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-validate ${PROF_ARGS:-} \
+    > gpurun_out/${TAG}_prof_bench.log 2>&1
+  rc=$?; echo "prof exit $rc"; if fatal $rc; then exit $rc; fi
+  cp "$(find gpurun_out/${TAG}_prof -name '*kernel_stats.csv' | head -1)" gpurun_out/${TAG}_kernel_stats.csv
+  find gpurun_out/${TAG}_prof -name '*kernel_trace.csv' -delete
 fi
 exit 0
