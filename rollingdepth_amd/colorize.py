@@ -59,10 +59,14 @@ def _launch(d: torch.Tensor, mn_rng, name: str, index: bool) -> torch.Tensor:
 
 
 def _as_device(depth, device) -> torch.Tensor:
+    """The device path evaluates the reference's index arithmetic in the depth's own dtype, f16 or
+    f32 (what the pipeline outputs).  Other dtypes are rejected rather than converted: the reference
+    computes (d − min) / (max − min) in float64 for float64 input, and an f32 evaluation could pick a
+    different colormap entry at a bin edge."""
     if isinstance(depth, np.ndarray):
         depth = torch.from_numpy(np.ascontiguousarray(depth))
     if depth.dtype not in (torch.float16, torch.float32):
-        depth = depth.float()
+        raise TypeError(f"colorize: depth dtype {depth.dtype} unsupported (float16 / float32; convert explicitly)")
     return depth.to(device)
 
 

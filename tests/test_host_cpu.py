@@ -237,3 +237,17 @@ def test_aligner_workspace_sizes_history_slots():
     assert _native.lib.rdmi_aligner_workspace(C.byref(a)) == with_hist
     a.iters = 10
     assert _native.lib.rdmi_aligner_workspace(C.byref(a)) < with_hist
+
+
+def test_colorize_rejects_float64():
+    """The device colouriser evaluates the reference's index arithmetic in f16 / f32; float64 depth
+    (which the reference normalises in float64) is refused instead of silently rounded (no GPU call:
+    the dtype check precedes any device work)."""
+    import numpy as np
+
+    from rollingdepth_amd import colorize as Cz
+
+    with pytest.raises(TypeError, match="float64"):
+        Cz.colorize_depth_multi_thread(np.zeros((1, 1, 4, 4)), device="cpu")
+    with pytest.raises(TypeError, match="float64"):
+        Cz.colorize_depth(np.zeros((1, 4, 4)), 0.0, 1.0, device="cpu")
