@@ -10,9 +10,12 @@ equal --gpus or the bench exits non-zero.
 
 Workload (default = BASELINE.json configs[1], the "fast" preset): synthetic 768×768 RGB video,
 dilations [1,25] (cap_dilation=True), snippet length 3, 1-step DDIM, fp16, no refine; SD2-shaped UNet
-(866 M) + KL-f8 VAE with random-init weights (no checkpoint offline).  Weak scaling by default: F=100
-frames per GPU (F·N frames at N GPUs); `--frames-total T` fixes the video length instead (strong
-scaling, e.g. the paper preset's 500 frames).  One step = the whole forward over the video (encode,
+(866 M) + KL-f8 VAE with random-init weights (no checkpoint offline).  Strong scaling by default: one
+100-frame video (the paper preset: 500 frames) split over the N GPUs — the multi-GPU question of
+BASELINE.json configs[4] is how fast one video gets done; `--frames F` runs F frames per GPU instead
+(weak scaling).  (With dilations [1, 25] the work per frame grows with the video length — the d = 25
+snippet count is N − 52 — so a weak-scaling curve mixes that growth with the communication cost:
+the algorithm alone caps 8-GPU weak-scaling efficiency near 0.77)  One step = the whole forward over the video (encode,
 every snippet's UNet step + 3 VAE decodes, 2000-iteration DepthAligner, merge, renormalise, refine
 when the preset has it) with the frames already resident in HBM, outputs copied to pinned host
 memory; at N > 1 shard.sharded_forward (snippet data parallel over RCCL).  value = frames processed
@@ -52,9 +55,9 @@ PEAK_HBM_GBS = 8000.0
 
 # run_video.py:413-452 presets (BASELINE.json configs[1..4])
 PRESETS = {
-    "fast": dict(res=768, dilations=[1, 25], refine=0, cap=True, dtype="f16", frames=100, frames_total=None),
-    "fast1024": dict(res=1024, dilations=[1, 25], refine=0, cap=True, dtype="f16", frames=100, frames_total=None),
-    "full": dict(res=1024, dilations=[1, 10, 25], refine=10, cap=True, dtype="f16", frames=100, frames_total=None),
+    "fast": dict(res=768, dilations=[1, 25], refine=0, cap=True, dtype="f16", frames=None, frames_total=100),
+    "fast1024": dict(res=1024, dilations=[1, 25], refine=0, cap=True, dtype="f16", frames=None, frames_total=100),
+    "full": dict(res=1024, dilations=[1, 10, 25], refine=10, cap=True, dtype="f16", frames=None, frames_total=100),
     "paper": dict(res=768, dilations=[1, 10, 25], refine=10, cap=False, dtype="f32", frames=None,
                   frames_total=500),
 }
@@ -225,12 +228,12 @@ def main():
     pr = dict(PRESETS[a.preset])
     res = a.res or pr["res"]
     dil0 = [int(x) for x in a.dilations.split(",")] if a.dilations else list(pr["dilations"])
-    if a.frames_total is not None or (a.frames is None and pr["frames_total"] is not None):
+    if a.frames is not None:
+        N = a.frames * world
+        scaling = "weak"
+    else:
         N = a.frames_total or pr["frames_total"]
         scaling = "strong"
-    else:
-        N = (a.frames or pr["frames"]) * world
-        scaling = "weak"
 
     if world > 1:
         torch.cuda.set_device(local)
