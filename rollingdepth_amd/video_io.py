@@ -1,7 +1,8 @@
 """Video ingest and egress — rollingdepth/video_io.py.
 
 Decoding and encoding need PyAV (absent from this image): `load_video_frames` on a path and
-`write_video_from_numpy` raise ImportError saying so.  Everything after the decode runs on the
+`write_video_from_numpy` raise ImportError saying so (the PyAV calls themselves are written and
+exercised against a stand-in module in tests/test_host_cpu.py).  Everything after the decode runs on the
 device: given decoded rgb24 frames (what PyAV's `frame.to_ndarray(format="rgb24")` returns,
 uint8 [N, H, W, 3] — numpy or torch), `load_video_frames` uploads the uint8 frames (a quarter of
 the PCIe bytes of the reference's float frames) and resizes + normalises them in one librdmi pass
@@ -88,16 +89,48 @@ def load_video_frames(input_path, start_frame: int = 0, frame_count: int = 0, pr
 
 def write_video_from_numpy(frames: np.ndarray, output_path, fps: int = 30, codec=None, crf: int = 23,
                            preset: str = "medium", verbose: bool = False) -> None:
-    """video_io.py:140-208 — encoding needs PyAV (absent from this image)."""
+    """video_io.py:140-208: uint8 rgb24 frames [n, H, W, 3] → a video file through PyAV (absent from
+    this image: ImportError).  Codec: the given one, else the first of libx264 / h264 / mpeg4 / mjpeg
+    that PyAV knows (ValueError when none does); yuv420p; crf / preset only for the x264 codecs; one
+    rgb24 frame per input frame, then the encoder flushed."""
     if len(frames.shape) != 4 or frames.shape[-1] != 3:
         raise ValueError(f"Expected shape [n, height, width, 3], got {frames.shape}")
     if frames.dtype != np.uint8:
         raise ValueError(f"Expected dtype uint8, got {frames.dtype}")
     try:
-        import av  # noqa: F401
+        import av
     except ImportError as e:
         raise ImportError("video encoding needs PyAV, which is not installed in this image") from e
-    raise NotImplementedError("video encoding (PyAV present but not wired in this build)")  # pragma: no cover
+    n, height, width, _ = frames.shape
+    candidates = [codec] if codec is not None else ["libx264", "h264", "mpeg4", "mjpeg"]
+    container = stream = chosen = None
+    for c in candidates:
+        container = av.open(output_path, mode="w")
+        try:
+            stream = container.add_stream(c, rate=fps)
+        except av.codec.codec.UnknownCodecError:
+            container.close()
+            continue
+        chosen = c
+        break
+    if chosen is None:
+        raise ValueError(f"No working codec found. Tried: {candidates}. Please install ffmpeg with necessary codecs.")
+    if verbose:
+        import logging
+
+        logging.info(f"Using codec: {chosen}")
+    try:
+        stream.width, stream.height, stream.pix_fmt = width, height, "yuv420p"
+        if chosen in ("libx264", "h264"):
+            stream.options = {"crf": str(crf), "preset": preset}
+        for i in range(n):
+            vf = av.VideoFrame.from_ndarray(np.ascontiguousarray(frames[i]), format="rgb24")
+            for packet in stream.encode(vf):
+                container.mux(packet)
+        for packet in stream.encode(None):  # flush the encoder
+            container.mux(packet)
+    finally:
+        container.close()
 
 
 def get_video_fps(video_path) -> float:

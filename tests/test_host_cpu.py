@@ -251,3 +251,79 @@ def test_colorize_rejects_float64():
         Cz.colorize_depth_multi_thread(np.zeros((1, 1, 4, 4)), device="cpu")
     with pytest.raises(TypeError, match="float64"):
         Cz.colorize_depth(np.zeros((1, 4, 4)), 0.0, 1.0, device="cpu")
+
+
+class _FakeAV:
+    """Stand-in for PyAV (absent from the image) recording what write_video_from_numpy asks of it:
+    the codec fallback, stream settings, every encoded frame and the flush."""
+
+    def __init__(self, known=("mpeg4", "mjpeg")):
+        import types
+
+        self.known, self.log, self.frames = set(known), [], []
+
+        class UnknownCodecError(Exception):
+            pass
+
+        self.codec = types.SimpleNamespace(codec=types.SimpleNamespace(UnknownCodecError=UnknownCodecError))
+        av = self
+
+        class Stream:
+            def encode(self, frame):
+                av.log.append(("encode", frame is None))
+                if frame is not None:
+                    av.frames.append(frame.arr.copy())
+                return [("packet", len(av.log))]
+
+        class Container:
+            def add_stream(self, codec, rate):
+                av.log.append(("add_stream", codec, rate))
+                if codec not in av.known:
+                    raise UnknownCodecError(codec)
+                av.stream = Stream()
+                return av.stream
+
+            def mux(self, packet):
+                av.log.append(("mux",))
+
+            def close(self):
+                av.log.append(("close",))
+
+        class VideoFrame:
+            @staticmethod
+            def from_ndarray(arr, format):
+                assert format == "rgb24"
+                return type("F", (), {"arr": arr})()
+
+        self.open = lambda path, mode="r": (self.log.append(("open", path, mode)), Container())[1]
+        self.VideoFrame = VideoFrame
+
+
+def test_write_video_from_numpy_against_a_pyav_stand_in(monkeypatch):
+    """video_io.py:140-208's encoder loop through a recording stand-in for PyAV: codec fallback past
+    the x264 codecs, yuv420p, no x264 options on mpeg4, one rgb24 frame per input in order, flush."""
+    import sys
+
+    import numpy as np
+
+    from rollingdepth_amd import video_io as V
+
+    fake = _FakeAV()
+    monkeypatch.setitem(sys.modules, "av", fake)
+    frames = (np.arange(3 * 4 * 6 * 3) % 251).astype(np.uint8).reshape(3, 4, 6, 3)
+    V.write_video_from_numpy(frames, "/tmp/out.mp4", fps=12)
+    tried = [e[1] for e in fake.log if e[0] == "add_stream"]
+    assert tried == ["libx264", "h264", "mpeg4"]
+    st = fake.stream
+    assert (st.width, st.height, st.pix_fmt) == (6, 4, "yuv420p") and not hasattr(st, "options")
+    assert len(fake.frames) == 3 and all(np.array_equal(a, b) for a, b in zip(fake.frames, frames))
+    enc = [e for e in fake.log if e[0] == "encode"]
+    assert enc[-1] == ("encode", True) and len(enc) == 4
+    assert fake.log[-1] == ("close",)
+    fake2 = _FakeAV(known=("libx264",))
+    monkeypatch.setitem(sys.modules, "av", fake2)
+    V.write_video_from_numpy(frames, "/tmp/out.mp4", crf=18, preset="fast")
+    assert fake2.stream.options == {"crf": "18", "preset": "fast"}
+    monkeypatch.setitem(sys.modules, "av", _FakeAV(known=()))
+    with pytest.raises(ValueError, match="No working codec"):
+        V.write_video_from_numpy(frames, "/tmp/out.mp4")

@@ -479,7 +479,9 @@ def _shard_worker(rank, world, port, name, dtype_name, res, seeded=False):
     # no explicit group: the world group, refine's all-reduce included (each rank runs only its own
     # refine snippets); seeded: no injected noise — rank 0 draws it from the caller's generator
     gen = torch.Generator(device="cuda").manual_seed(123) if seeded else None
-    so = sharded_forward(pipe, t["frames"][None].cuda(), list(meta["dilations_in"]), True, 3, None,
+    slens = list(meta.get("snippet_lengths", [3]))
+    so = sharded_forward(pipe, t["frames"][None].cuda(), list(meta["dilations_in"]), True,
+                         slens if len(slens) > 1 else slens[0], None,
                          init_noise=None if seeded else t["init_noise"].cuda(), refine_step=rs,
                          refine_start_dilation=rsd, gather=True, generator=gen)
     torch.cuda.synchronize()
@@ -490,7 +492,7 @@ def _shard_worker(rank, world, port, name, dtype_name, res, seeded=False):
         pipe.snippet_batch = 8
         seen.clear()
         gen1 = torch.Generator(device="cuda").manual_seed(123) if seeded else None
-        out = pipe.forward(t["frames"][None], list(meta["dilations_in"]), True, [3], [1], [1], None, rs, 3, rsd, gen1,
+        out = pipe.forward(t["frames"][None], list(meta["dilations_in"]), True, slens, [1], [1], None, rs, 3, rsd, gen1,
                            False, 4, False, init_noise=None if seeded else t["init_noise"])
         d = (so.depth_pred_full.float().cpu() - out.depth_pred.float()).abs().mean().item()
         dref = 0.0 if seeded else (so.depth_pred_full.float().cpu() - t["depth_pred"]).abs().mean().item()
@@ -505,7 +507,8 @@ def _shard_worker(rank, world, port, name, dtype_name, res, seeded=False):
 @pytest.mark.parametrize("name,dtype_name,world,seeded", [("tiny_pipeline", "float16", 2, False),
                                                           ("tiny_refine", "float16", 3, False),
                                                           ("tiny_refine", "float32", 2, False),
-                                                          ("tiny_refine", "float16", 2, True)])
+                                                          ("tiny_refine", "float16", 2, True),
+                                                          ("tiny_mixed", "float16", 2, False)])
 def test_sharded_forward_multi_rank_one_gpu(name, dtype_name, world, seeded):
     """The multi-rank plan with the real kernels: W ranks on the one GPU of the box, collectives over
     gloo (device tensors staged through host memory — RCCL needs one GPU per rank), outputs

@@ -143,3 +143,42 @@ def test_concatenate_videos_horizontally(dtype):
         assert (out.int() - ref.int()).abs().max().item() <= 1
     else:
         assert (out - ref).abs().max().item() <= 1e-3
+
+
+def test_load_video_frames_decode_path_against_a_pyav_stand_in(monkeypatch):
+    """video_io.py:71-137's decode loop (PyAV is absent: a stand-in container yields rgb24 frames):
+    start_frame / frame_count select the same frames the reference keeps, thread_type is set, the
+    container is closed, and the result equals the decoded-frames entry point's; get_video_fps reads
+    average_rate (video_io.py:211-224)."""
+    import sys
+    import types
+
+    from rollingdepth_amd import video_io as V
+
+    raw = _frames(7, 40, 56, seed=3)
+    closed = []
+
+    class Frame:
+        def __init__(self, a):
+            self.a = a
+
+        def to_ndarray(self, format):
+            assert format == "rgb24"
+            return self.a
+
+    class Container:
+        def __init__(self):
+            self.streams = types.SimpleNamespace(video=[types.SimpleNamespace(thread_type=None, average_rate=24.0)])
+
+        def decode(self, stream):
+            assert stream.thread_type == "AUTO"
+            return (Frame(f) for f in raw)
+
+        def close(self):
+            closed.append(True)
+
+    monkeypatch.setitem(sys.modules, "av", types.SimpleNamespace(open=lambda path: Container()))
+    got, hw = V.load_video_frames("/in.mp4", start_frame=2, frame_count=3, processing_res=32, device="cuda")
+    want, hw2 = V.frames_from_rgb24(raw[2:5], 32, "BILINEAR", device="cuda")
+    assert hw == hw2 == (40, 56) and closed and torch.equal(got, want)
+    assert V.get_video_fps("/in.mp4") == 24.0
