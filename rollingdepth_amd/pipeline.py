@@ -296,14 +296,17 @@ class RollingDepthPipeline:
         return out
 
     def _vae_chunks(self, n: int, h: int, w: int) -> List[Tuple[int, int]]:
-        """Balanced VAE chunks of at most vae_batch frames, capped so that the mid-block attention's
-        f32 scores ([b, h·w, h·w]) stay ≤ 32 GB and one full-resolution 128-channel activation ≤ 24 GB
-        (768²: 75 frames; 1024²: 30).  Measured at 768² (75-frame snippet batches): 16 → 21.0,
-        38 → 21.1, 75 → 21.2 depth frames/s (profiles/r01_vae_batch_ab.log)."""
+        """Balanced VAE chunks of at most vae_batch frames, capped so that one full-resolution
+        128-channel activation stays ≤ 24 GB and — where the mid-block attention materialises its f32
+        scores ([b, h·w, h·w]: the f32 path, or RDMI_VAE_FLASH=0) — the scores ≤ 32 GB.  The f16 flash
+        kernel (attention_d512.hip) holds no scores, so f16 chunks are not capped by them (768²: 75
+        frames, 1024²: 75 — the scores cap was 62 / 19).  Measured at 768² (75-frame snippet
+        batches, round 1): 16 → 21.0, 38 → 21.1, 75 → 21.2 depth frames/s (profiles/r01_vae_batch_ab.log)."""
         hw = h * w
         esz = self.dtype.itemsize  # (f32 path: the probabilities are f32 too, and every activation doubles)
-        cap = min(self.vae_batch, max(1, int(32e9 // (hw * hw * (4 + esz)))),
-                  max(1, int(24e9 // (hw * 64 * 128 * esz))))
+        cap = min(self.vae_batch, max(1, int(24e9 // (hw * 64 * 128 * esz))))
+        if self.dtype == F32 or os.environ.get("RDMI_VAE_FLASH", "1") == "0":
+            cap = min(cap, max(1, int(32e9 // (hw * hw * (4 + esz)))))
         return _balanced(n, cap)
 
     def decode_depth(self, z_scaled: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
