@@ -51,6 +51,9 @@ sys.path.insert(0, ROOT)
 
 PEAK_F16_TFLOPS = 2500.0  # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_F32_TFLOPS = 157.3   # MI355X f32-input MFMA (= f32 vector peak)
+# the bf16-split f32 engine (RDMI_F32_X3) spends three bf16 MFMA products per f32 multiply-add: its
+# ceiling in f32 flops is the bf16 peak / 3
+PEAK_F32X3_TFLOPS = PEAK_F16_TFLOPS / 3
 PEAK_HBM_GBS = 8000.0
 
 # run_video.py:413-452 presets (BASELINE.json configs[1..4])
@@ -322,7 +325,8 @@ def main():
         dom = max(prof, key=lambda k: prof[k]["ms"])
         p = prof[dom]
         ach = _fam(dom)
-        peak = PEAK_F32_TFLOPS if dom.endswith("_f32") else PEAK_F16_TFLOPS
+        peak = (PEAK_F32_TFLOPS if dom.endswith("_f32") else PEAK_F32X3_TFLOPS if dom.endswith("_f32x3")
+                else PEAK_F16_TFLOPS)
         tr = _pmc_traffic(a.preset, dom)
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": tr and round(tr["bytes_per_launch"]),
@@ -344,7 +348,8 @@ def main():
             "metric": "depth frames/sec at 768px snip_len=3, 1-step denoise; 1/2/4/8 MI355X",
             "value": round(total_frames / dt, 4), "unit": "depth frames/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 1), "higher_is_better": True,
-            "scaling": scaling, "vs_baseline": None, "dtype": pr["dtype"], "data": "synthetic",
+            "scaling": scaling, "vs_baseline": None, "data": "synthetic",
+            "dtype": pr["dtype"] + (" (bf16x3 products)" if pr["dtype"] == "f32" and K.f32_x3() else ""),
             "config": {"workload": f"{a.preset} preset: {N}-frame {res}x{res} video, dilations {dil0} "
                                    f"(cap_dilation={pr['cap']}), snippet_len 3, 1-step DDIM, aligner "
                                    f"{a.aligner_iters} it, refine {refine}; SD2-shaped UNet+VAE random-init",

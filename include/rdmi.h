@@ -34,6 +34,10 @@ extern "C" {
 #define RDMI_F16 0
 #define RDMI_F32 1
 #define RDMI_U8 2 /* decoded video frames (rdmi_resize input) */
+/* rdmi_gemm / rdmi_conv2d only: f32 activations and output, weights pre-split into bf16 hi/lo parts,
+ * products a_hi·w_hi + a_hi·w_lo + a_lo·w_hi on the bf16 MFMA with f32 accumulation (≈2^-16 relative
+ * error per product; the paper preset's fast f32 engine, RDMI_F32_X3=1 in rollingdepth_amd) */
+#define RDMI_F32_X3 3
 
 /* rdmi_resize modes: torchvision InterpolationMode NEAREST / BILINEAR / BICUBIC */
 #define RDMI_RESIZE_NEAREST 0
@@ -75,7 +79,9 @@ typedef struct rdmi_gemm_args {
   float* gn_part; long gn_ld;
   /* storage dtype of A, W, C and residual: RDMI_F16 (f16 MFMA, f32 accumulate; C f32 when c_f32) or
    * RDMI_F32 (the paper preset: f32-input MFMA v_mfma_f32_16x16x4_f32, exact f32 products, C / residual
-   * f32; K % 4 == 0; no GroupNorm moments) */
+   * f32; K % 4 == 0; no GroupNorm moments) or RDMI_F32_X3 (as RDMI_F32, W the bf16 split layout:
+   * row n holds, per 32-deep K-tile t, bf16(w[n, 32t..32t+31]) then bf16(w − that), so ldw / strideW
+   * count bf16 elements, ldw % 64 == 0 and ldw ≥ 2·ceil(K/32)·32) */
   int dtype;
 } rdmi_gemm_args;
 int rdmi_gemm(const rdmi_gemm_args* args, void* stream);
@@ -107,7 +113,8 @@ typedef struct rdmi_conv_args {
    * Shapes that support it: rdmi_conv2d_in_gn_supported (otherwise RDMI_E_UNSUPPORTED). */
   const float* in_mean_rstd; const float* in_gamma; const float* in_beta; int in_groups, in_silu;
   /* RDMI_F16 or RDMI_F32 (x, w, y, residual).  f32 weights are always [Cout][kh][kw][Cin] (tap-major,
-   * Kp % 32 == 0), Cin % 4 == 0, no input GroupNorm and no GroupNorm moments. */
+   * Kp % 32 == 0), Cin % 4 == 0, no input GroupNorm and no GroupNorm moments.  RDMI_F32_X3: f32 x, y,
+   * residual; w in the bf16 split layout that rdmi_gemm_args describes, rows of 2·Kp bf16 (Kp still counts f32 K). */
   int dtype;
   /* Optional, upsample = 1 only: the same conv's weights for the phase-decomposed form — the ×2
    * nearest upsample + 3×3 conv computed as four 2×2 convs on the source grid, one per output

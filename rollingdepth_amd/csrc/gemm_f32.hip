@@ -14,7 +14,19 @@
 // fragment instead of eight 4-B reads; the sum over k is the same set of products.
 // The MFMA runs as Dᵀ = W·Aᵀ, so a lane holds 4 consecutive output channels of one output row
 // (the f16 engine's epilogue geometry): bias / residual / output move as 16-B vectors.
+//
+// X3 (dtype RDMI_F32_X3): the same engine with the products on the bf16 MFMA, 16× the f32 rate.
+// Every f32 operand is split into two bf16 parts, x = x_hi + x_lo + O(2^-17 |x|) (x_hi = bf16(x),
+// x_lo = bf16(x − x_hi); the weights once at load, the activations as their fragments leave LDS),
+// and a·w is formed as a_hi·w_hi + a_hi·w_lo + a_lo·w_hi with f32 accumulation: three
+// v_mfma_f32_16x16x32_bf16 per 32-deep K step in place of eight v_mfma_f32_16x16x4_f32.  The dropped
+// a_lo·w_lo and the two splits leave ≈2^-16 relative error per product (about 2^-24 for exact f32,
+// 2^-11 for the TF32 that cuDNN's fp32 convolutions use by default on the reference's Ampere GPU).
+// The weight rows hold, per 32-deep K-tile, 32 bf16 hi then 32 bf16 lo values — 128 B, the byte
+// geometry of the f32 engine's K-tile, so the DMA and its swizzle are unchanged.
 #include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 namespace {
 
@@ -126,9 +138,26 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
   }
 }
 
+// 8 f32 values → their bf16 hi and lo parts (round-to-nearest-even both times); x_hi + x_lo is x to
+// ≈2^-17 relative.  v_cvt_pk_bf16_f32 puts its first operand in the low half.
+__device__ __forceinline__ void split_bf16x8(const f32x4& a0, const f32x4& a1, bf16x8& hi, bf16x8& lo) {
+  const float x[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+  unsigned h[4], l[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h[t]) : "v"(x[2 * t]), "v"(x[2 * t + 1]));
+    const float h0 = __builtin_bit_cast(float, h[t] << 16), h1 = __builtin_bit_cast(float, h[t] & 0xffff0000u);
+    const float r0 = x[2 * t] - h0, r1 = x[2 * t + 1] - h1;
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(l[t]) : "v"(r0), "v"(r1));
+  }
+  hi = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) unsigned){h[0], h[1], h[2], h[3]});
+  lo = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) unsigned){l[0], l[1], l[2], l[3]});
+}
+
 // MODE 0: dense A [M, K]; MODE 1: implicit im2col of an NHWC f32 tensor for a 3×3 conv (any stride /
 // padding, K order [tap][Cin]); MODE 2: the 3×3 conv reading x through a nearest ×2 upsample.
-template <int MODE>
+// X3: bf16-split products (header).
+template <int MODE, bool X3>
 __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
   constexpr int BM = 128, BN = 128, NW = 4, WTM = 64, WTN = 64;
   constexpr int RM = WTM / 16, RN = WTN / 16;
@@ -217,7 +246,8 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      const bool ok = brow[i] >= 0 && kok;
+      // X3: a K-tile of W is 32 hi then 32 lo bf16, always whole (zero padded past K)
+      const bool ok = brow[i] >= 0 && (X3 || kok);
       dma16f(rw_, ok ? (unsigned)(brow[i] + kk) * 4u : OOB, lb + (i * NW + wid) * 8 * BKF);
     }
   };
@@ -240,6 +270,33 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
     issue(kt + 2, (kt + 2) % 3);
     const float* la = lds + (kt % 3) * SLOT + (wm * WTM) * BKF;
     const float* lb = lds + (kt % 3) * SLOT + BM * BKF + (wn * WTN) * BKF;
+    if constexpr (X3) {
+      // lane quarter fq holds k = 8fq .. 8fq+7 of its row in both operands (the bf16 16x16x32 layout):
+      // A as f32 chunks 2fq, 2fq+1 (split here), W as bf16 chunks fq (hi) and 4+fq (lo)
+      bf16x8 ah[RM], al[RM], bh[RN], bl[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int row = i * 16 + fr;
+        const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ (row & 7)) << 2));
+        const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ (row & 7)) << 2));
+        split_bf16x8(a0, a1, ah[i], al[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int row = j * 16 + fr;
+        bh[j] = *(const bf16x8*)(lb + row * BKF + ((fq ^ (row & 7)) << 2));
+        bl[j] = *(const bf16x8*)(lb + row * BKF + (((4 + fq) ^ (row & 7)) << 2));
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], ah[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh[j], al[i], acc[i][j], 0, 0, 0);
+        }
+      continue;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int lc = 2 * fq + h;  // logical chunk: k = 8·fq + 4h + (0..3)
@@ -277,17 +334,24 @@ bool vec_ok(const GemmF32P& p) {
   return ok;
 }
 
-int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode) {
+int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode, bool x3) {
   const char* gm = getenv("RDMI_GEMM_GROUP");
   p.group_m = gm ? atoi(gm) : 8;
   dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
-  if (mode == 2)
-    hipLaunchKernelGGL(gemm_f32_kernel<2>, g, dim3(256), 0, s, p);
-  else if (mode == 1)
-    hipLaunchKernelGGL(gemm_f32_kernel<1>, g, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(gemm_f32_kernel<0>, g, dim3(256), 0, s, p);
-  return rdmi::check_launch("gemm_f32");
+#define RDMI_F32_LAUNCH(M)                                                                     \
+  if (x3)                                                                                      \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, true>), g, dim3(256), 0, s, p);                    \
+  else                                                                                         \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, false>), g, dim3(256), 0, s, p);
+  if (mode == 2) {
+    RDMI_F32_LAUNCH(2)
+  } else if (mode == 1) {
+    RDMI_F32_LAUNCH(1)
+  } else {
+    RDMI_F32_LAUNCH(0)
+  }
+#undef RDMI_F32_LAUNCH
+  return rdmi::check_launch(x3 ? "gemm_f32x3" : "gemm_f32");
 }
 
 }  // namespace
@@ -295,18 +359,23 @@ int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode) {
 namespace rdmi {
 
 int gemm_f32(const rdmi_gemm_args* a, void* stream) {
-  RDMI_REQUIRE(a->K % 4 == 0 && a->lda % 4 == 0 && a->ldw % 4 == 0 && a->ldw >= a->K, RDMI_E_ALIGN,
-               "gemm f32: K (%d), lda (%ld), ldw (%ld) must be multiples of 4 (ldw >= K)", a->K, a->lda, a->ldw);
+  const bool x3 = a->dtype == RDMI_F32_X3;
+  // X3: W is the bf16 split layout, ldw in bf16 elements (2 per f32 K position)
+  const long ldw = x3 ? a->ldw / 2 : a->ldw;
+  RDMI_REQUIRE(!x3 || (a->ldw % 64 == 0), RDMI_E_ALIGN, "gemm f32x3: ldw (%ld bf16) must be a multiple of 64", a->ldw);
+  const int Kt = (a->K + BKF - 1) / BKF * BKF;
+  RDMI_REQUIRE(a->K % 4 == 0 && a->lda % 4 == 0 && ldw % 4 == 0 && ldw >= (x3 ? Kt : a->K), RDMI_E_ALIGN,
+               "gemm f32: K (%d), lda (%ld), ldw (%ld) must be multiples of 4 (ldw >= K)", a->K, a->lda, ldw);
   RDMI_REQUIRE(al16(a->A) && al16(a->W) && a->strideA % 4 == 0 && a->strideW % 4 == 0, RDMI_E_ALIGN,
                "gemm f32: A/W not 16-byte aligned");
   RDMI_REQUIRE(a->epilogue != RDMI_EPI_GEGLU || a->N % 128 == 0, RDMI_E_ARG, "gemm f32: GEGLU needs N %% 128 == 0");
   RDMI_REQUIRE(!a->rowbias || a->rows_per_group > 0, RDMI_E_ARG, "gemm f32: rowbias needs rows_per_group");
   RDMI_REQUIRE(!a->gn_part, RDMI_E_UNSUPPORTED, "gemm f32: no GroupNorm moments (the groupnorm pass computes them)");
-  RDMI_REQUIRE((long)a->M * a->lda < (1L << 29) && (long)a->N * a->ldw < (1L << 29), RDMI_E_ARG,
+  RDMI_REQUIRE((long)a->M * a->lda < (1L << 29) && (long)a->N * ldw < (1L << 29), RDMI_E_ARG,
                "gemm f32: operand exceeds 2^29 elements (2 GiB) per batch");
   GemmF32P p{};
   p.A = (const float*)a->A; p.lda = a->lda; p.sA = a->strideA;
-  p.Wt = (const float*)a->W; p.ldw = a->ldw; p.sW = a->strideW;
+  p.Wt = (const float*)a->W; p.ldw = ldw; p.sW = x3 ? a->strideW / 2 : a->strideW;
   p.C = (float*)a->C; p.ldc = a->ldc; p.sC = a->strideC;
   p.bias = a->bias; p.R = (const float*)a->residual; p.ldr = a->ldr; p.sR = a->strideR;
   p.rowbias = a->rowbias; p.rpg = a->rows_per_group > 0 ? a->rows_per_group : 1; p.rb_ld = a->rowbias_ld;
@@ -317,14 +386,16 @@ int gemm_f32(const rdmi_gemm_args* a, void* stream) {
   p.vec = vec_ok(p);
   RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm f32: GEGLU output needs 4-element aligned rows");
   p.a_bytes = (unsigned)(((long)(a->M - 1) * a->lda + a->K) * 4);
-  p.w_bytes = (unsigned)(((long)(a->N - 1) * a->ldw + a->K) * 4);
-  return launch_f32(p, a->batch, (hipStream_t)stream, 0);
+  p.w_bytes = (unsigned)(((long)(a->N - 1) * ldw + (x3 ? Kt : a->K)) * 4);
+  return launch_f32(p, a->batch, (hipStream_t)stream, 0, x3);
 }
 
 int conv2d_f32(const rdmi_conv_args* a, void* stream) {
+  const bool x3 = a->dtype == RDMI_F32_X3;  // Kp counts f32 K positions (the bf16 rows are 2·Kp long)
   RDMI_REQUIRE(a->Cin % 4 == 0, RDMI_E_ALIGN, "conv2d f32: Cin (%d) must be a multiple of 4", a->Cin);
   const int K = a->kh * a->kw * a->Cin;
-  RDMI_REQUIRE(a->Kp >= K && a->Kp % 4 == 0, RDMI_E_ARG, "conv2d f32: Kp (%d) must be >= %d, a multiple of 4", a->Kp, K);
+  RDMI_REQUIRE(a->Kp >= K && a->Kp % (x3 ? 32 : 4) == 0, RDMI_E_ARG, "conv2d f32: Kp (%d) must be >= %d, a multiple of %d",
+               a->Kp, K, x3 ? 32 : 4);
   RDMI_REQUIRE(al16(a->x) && al16(a->w), RDMI_E_ALIGN, "conv2d f32: x/w not 16-byte aligned");
   RDMI_REQUIRE((long)a->B * a->H * a->W * a->Cin < (1L << 29) && (long)a->Cout * a->Kp < (1L << 29), RDMI_E_ARG,
                "conv2d f32: input exceeds 2^29 elements (2 GiB; split the batch)");
@@ -347,7 +418,7 @@ int conv2d_f32(const rdmi_conv_args* a, void* stream) {
   p.vec = vec_ok(p);
   p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 4);
   p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 4);
-  return launch_f32(p, 1, (hipStream_t)stream, dense ? 0 : (a->upsample ? 2 : 1));
+  return launch_f32(p, 1, (hipStream_t)stream, dense ? 0 : (a->upsample ? 2 : 1), x3);
 }
 
 }  // namespace rdmi

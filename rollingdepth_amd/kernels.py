@@ -90,13 +90,48 @@ def _need_act(t: torch.Tensor, name: str):
 
 
 # ----------------------------------------------------------------------------- weight packing
+BF16 = torch.bfloat16
+
+
+def f32_x3() -> bool:
+    """Whether f32 weights are packed for the bf16-split engine (RDMI_F32_X3, rdmi.h; the default):
+    f32 activations and accumulation, three bf16 MFMA products per multiply-add (≈2^-16 relative per
+    product, 2.2× the exact engine's speed on the paper preset's shapes: profiles/r03f_x3_probe.log).
+    The reference's fp32 preset runs its convolutions through cuDNN with PyTorch's default
+    allow_tf32 (run_video.py sets no precision flag), i.e. with 2^-11 products on its Ampere+ GPUs.
+    RDMI_F32_X3=0 keeps exact f32 products (v_mfma_f32_16x16x4_f32).  Read at pack time."""
+    return os.environ.get("RDMI_F32_X3", "1") == "1"
+
+
+def split_bf16(w: torch.Tensor) -> torch.Tensor:
+    """f32 [N, Kp] (Kp % 32 == 0) → bf16 [N, 2·Kp]: per 32-deep K-tile, bf16(w) then bf16(w − bf16(w))
+    (both round-to-nearest-even; the RDMI_F32_X3 weight layout of rdmi.h)."""
+    n, kp = w.shape
+    if kp % 32:
+        raise ValueError(f"split_bf16: K {kp} not a multiple of 32")
+    hi = w.to(BF16)
+    lo = (w - hi.float()).to(BF16)
+    return torch.stack((hi.view(n, kp // 32, 32), lo.view(n, kp // 32, 32)), 2).reshape(n, 2 * kp).contiguous()
+
+
 def pack_linear(w: torch.Tensor, device, dtype=F16) -> torch.Tensor:
-    """[N, K] → [N, Kp] in the storage dtype (K zero-padded to a multiple of 32)."""
+    """[N, K] → [N, Kp] in the storage dtype (K zero-padded to a multiple of 32); f32 with
+    f32_x3(): split_bf16 of that ([N, 2·Kp] bf16)."""
     n, k = w.shape
     kp = (k + 31) // 32 * 32
     out = torch.zeros((n, kp), dtype=dtype, device=device)
     out[:, :k] = w.to(device=device, dtype=dtype)
-    return out
+    return split_bf16(out) if dtype == F32 and f32_x3() else out
+
+
+def _w_code(a: torch.Tensor, w: torch.Tensor, name: str) -> int:
+    """dtype code of a GEMM/conv: the activations' dtype, or RDMI_F32_X3 for f32 activations
+    against split_bf16 weights."""
+    if a.dtype == F32 and w.dtype == BF16:
+        _need(w, BF16, name)
+        return _N.RDMI_F32_X3
+    _need(w, a.dtype, name)
+    return _N.RDMI_F32 if a.dtype == F32 else _N.RDMI_F16
 
 
 def geglu_permute(w: torch.Tensor, b: torch.Tensor):
@@ -120,7 +155,8 @@ def pad_channels(c: int) -> int:
 def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16) -> torch.Tensor:
     """[Cout, Cin, kh, kw] → [Cout, Kp] in the implicit-GEMM K order of gemm.hip (rdmi.h): f16:
     [Cout][Cin_pad/64][kh][kw][64] when kh·kw > 1 and Cin_pad % 64 == 0, else [Cout][kh][kw][Cin_pad];
-    f32 (gemm_f32.hip): always [Cout][kh][kw][Cin_pad]; zero padded to Kp % 32 == 0."""
+    f32 (gemm_f32.hip): always [Cout][kh][kw][Cin_pad]; zero padded to Kp % 32 == 0 (with f32_x3():
+    split_bf16 of that)."""
     co, ci, kh, kw = w.shape
     cp = cin_pad or pad_channels(ci)
     t = torch.zeros((co, kh, kw, cp), dtype=F32)
@@ -131,6 +167,8 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16)
     kp = (k + 31) // 32 * 32
     out = torch.zeros((co, kp), dtype=dtype)
     out[:, :k] = t.reshape(co, k).to(dtype)
+    if dtype == F32 and f32_x3():
+        out = split_bf16(out)
     return out.to(device)
 
 
@@ -169,7 +207,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     gn=True: the epilogue also emits the GroupNorm moments of the output (see _gn_part), which a
     following `groupnorm(out, ...)` consumes instead of re-reading the tensor."""
     _need_act(a, "gemm.a")
-    _need(w, a.dtype, "gemm.w")
+    code = _w_code(a, w, "gemm.w")
     f32 = a.dtype == F32
     out_f32 = out_f32 or f32
     batch = a.shape[0] if a.dim() == 3 else 1
@@ -182,7 +220,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     if residual is not None and residual.dtype != a.dtype:
         raise TypeError("gemm: residual dtype must match the activations")
     g = _gemm_args(a, w, out, bias, residual, rowbias, rows_per_group, alpha, M, N, k, batch, geglu, out_f32)
-    g.dtype = _N.RDMI_F32 if f32 else _N.RDMI_F16
+    g.dtype = code
     if silu:
         g.epilogue = 2
     part = _gn_part(out, M, N) if (gn and batch == 1 and not geglu and not out_f32) else None
@@ -192,7 +230,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     nb = es * (batch * M * k + (batch if w.dim() == 3 else 1) * N * k) + out.element_size() * batch * M * NO
     if residual is not None:
         nb += es * batch * M * NO
-    with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * M * N * k * batch,
+    with _Timed(_engine_name(code), 2.0 * M * N * k * batch,
                 f"gemm M={M} N={N} K={k} b={batch}", nb):
         check(lib.rdmi_gemm(C.byref(g), _stream()), "rdmi_gemm")
     _gn_attach(out, part)
@@ -220,6 +258,10 @@ def gn_view(t: torch.Tensor, shape) -> torch.Tensor:
     v = t.view(shape)
     _gn_attach(v, getattr(t, _GN_ATTR, None))
     return v
+
+
+def _engine_name(code: int) -> str:
+    return {_N.RDMI_F16: "implicit_gemm", _N.RDMI_F32: "implicit_gemm_f32", _N.RDMI_F32_X3: "implicit_gemm_f32x3"}[code]
 
 
 def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, geglu, out_f32):
@@ -288,7 +330,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     in_gn=(mean_rstd, gamma, beta, groups, silu): GroupNorm(+SiLU) of x applied as it is read
     (rdmi.h rdmi_conv_args.in_*; only where conv2d_in_gn_supported)."""
     _need_act(x, "conv2d.x")
-    _need(w, x.dtype, "conv2d.w")
+    code = _w_code(x, w, "conv2d.w")
     f32 = x.dtype == F32
     B, H, W, Cin = x.shape
     Ho, Wo = _out_hw(H, W, k, stride, pad, upsample, out_hw)
@@ -320,8 +362,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
                    out[s0:s1], alpha, out_hw, in_gn=ig, _gn_slot=slot, w_up2=w_up2)
         _gn_attach(out, part)
         return out
-    if w.shape[1] < k * k * Cin:
-        raise ValueError(f"conv2d: packed weight K {w.shape[1]} < {k * k * Cin}")
+    kp = w.shape[1] // 2 if code == _N.RDMI_F32_X3 else w.shape[1]
+    if kp < k * k * Cin:
+        raise ValueError(f"conv2d: packed weight K {kp} < {k * k * Cin}")
     if w_up2 is not None and (f32 or os.environ.get("RDMI_UP2", "0") != "1"):
         w_up2 = None  # opt-in: see DESIGN.md §7 (same accuracy in expectation, but the 768² depth
         # parity sits on the min/max renormalisation of two pixels — tools/depth_sensitivity.py)
@@ -330,7 +373,8 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
         raise ValueError(f"conv2d: w_up2 must be pack_conv_up2's [4, {cout}, {4 * Cin}] f16")
     a = _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn,
                    w_up2)
-    a.dtype = _N.RDMI_F32 if f32 else _N.RDMI_F16
+    a.dtype = code
+    a.Kp = kp
     if part is not None:
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
@@ -341,7 +385,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     taps = 4 if (w_up2 is not None and _up2_runs(a)) else k * k
     nb = es * (x.numel() + cout * (16 if taps == 4 else k * k) * Cin +
                (2 if residual is not None else 1) * B * Ho * Wo * cout)
-    with _Timed("implicit_gemm_f32" if f32 else "implicit_gemm", 2.0 * B * Ho * Wo * cout * taps * Cin,
+    with _Timed(_engine_name(code), 2.0 * B * Ho * Wo * cout * taps * Cin,
                 f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}",
                 nb):
         check(lib.rdmi_conv2d(C.byref(a), _stream()), "rdmi_conv2d")

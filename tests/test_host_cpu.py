@@ -69,6 +69,26 @@ def test_pack_conv_channel_block_major():
     assert torch.equal(K.pack_conv(w1, "cpu").float(), w1[:, :, 0, 0].half().float())
 
 
+def test_split_bf16_layout(monkeypatch):
+    """RDMI_F32_X3 weights (rdmi.h): per 32-deep K-tile, 32 bf16 hi then 32 bf16 lo; hi + lo is the
+    f32 weight to ≈2^-17 relative; zero K padding stays zero in both parts."""
+    from rollingdepth_amd import kernels as K
+
+    w = torch.randn(6, 70) * torch.logspace(-3, 3, 70)
+    monkeypatch.setenv("RDMI_F32_X3", "0")
+    f = K.pack_linear(w, "cpu", torch.float32)
+    monkeypatch.setenv("RDMI_F32_X3", "1")
+    p = K.pack_linear(w, "cpu", torch.float32)
+    assert f.shape == (6, 96) and p.shape == (6, 192) and p.dtype == torch.bfloat16
+    t = p.view(6, 3, 2, 32).float()
+    hi, lo = t[:, :, 0].reshape(6, 96), t[:, :, 1].reshape(6, 96)
+    assert torch.equal(hi, f.to(torch.bfloat16).float())
+    assert ((hi + lo - f).abs() <= f.abs() * 2.0 ** -16).all()
+    assert hi[:, 70:].abs().max() == 0 and lo[:, 70:].abs().max() == 0
+    c = K.pack_conv(torch.randn(4, 40, 3, 3), "cpu", 40, torch.float32)
+    assert c.dtype == torch.bfloat16 and c.shape == (4, 2 * 384)
+
+
 def test_pack_conv_up2_phase_identity():
     """pack_conv_up2: conv3×3(nearest×2(x)) == the four 2×2 phase convs on the source grid
     (rdmi.h rdmi_conv_args.w_up2) — the identity the GPU's phase-decomposed upsample relies on,
