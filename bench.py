@@ -335,7 +335,8 @@ def main():
                 "avg_launch_us": round(p["ms"] * 1e3 / max(p["n"], 1), 2),
                 "per_kernel": {k: {"tflops": round(_fam(k), 1), "ms": round(v["ms"], 1), "launches": v["n"]}
                                for k, v in prof.items()}}
-        for an, apk in (("attention_fwd", PEAK_F16_TFLOPS), ("attention_fwd_f32", PEAK_F32_TFLOPS)):
+        for an, apk in (("attention_fwd", PEAK_F16_TFLOPS), ("attention_fwd_f32", PEAK_F32_TFLOPS),
+                        ("attention_fwd_f32x3", PEAK_F32X3_TFLOPS)):
             if an in prof:
                 att = _fam(an)
                 roof["attention"] = {"kernel": an, "achieved": round(att, 1), "peak": apk, "unit": "TFLOP/s",

@@ -167,7 +167,8 @@ int rdmi_layernorm(const void* x, void* y, int dtype, long M, int C, const float
 
 /* ---------------------------------------------------------------------------------------
  * Fused multi-head attention forward, softmax(q kᵀ · scale) v, non-causal, no mask, D = 64; dtype
- * RDMI_F16 (f16 MFMA, f32 softmax) or RDMI_F32 (f32-input MFMA, f32 softmax; the paper preset).
+ * RDMI_F16 (f16 MFMA, f32 softmax), RDMI_F32 (f32-input MFMA, f32 softmax; the paper preset) or
+ * RDMI_F32_X3 (f32 q/k/v/o and softmax, both products as bf16-split triples on the bf16 MFMA).
  * Token-major q/k/v/o with row strides (ld*) and batch strides (bs*), head h at column h*D.
  * With the num_view fold done by the caller's strides (one "batch" = one snippet of n frames,
  * S = n·h·w), this is the cross-frame self-attention of the modified AttnProcessor2_0

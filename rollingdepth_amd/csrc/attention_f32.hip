@@ -1,5 +1,6 @@
 // f32 cross-frame flash attention (the paper preset's fp32 SDPA, attention_processor.py:2251-2253,
-// behind rdmi_attention_fwd with dtype RDMI_F32).  head_dim 64, non-causal, no mask.
+// behind rdmi_attention_fwd with dtype RDMI_F32, exact products; RDMI_F32_X3: bf16-split products,
+// attn_fwd_f32x3 below).  head_dim 64, non-causal, no mask.
 //
 // gfx950 runs f32 matrix products only on v_mfma_f32_16x16x4_f32 (exact f32, 1/16 of the f16 rate),
 // so this kernel is MFMA-bound by a wide margin and its design goal is to keep the matrix pipe fed:
@@ -194,19 +195,219 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32(AttnF32P p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// X3 form (dtype RDMI_F32_X3): the same flash schedule with both products on
+// v_mfma_f32_16x16x32_bf16 as bf16-split triples (a·b ≈ a_hi·b_hi + a_lo·b_hi + a_hi·b_lo, rdmi.h):
+// 6 bf16 MFMAs per 16×16×64 block where the exact form spends 16 f32 ones (each twice as long).
+//   * K and V are split once per workgroup as the tiles are staged: K as [key][d] hi and lo planes
+//     (128-B rows, 16-B chunks XOR-swizzled by key & 7), V transposed into [d][key] hi and lo planes
+//     (row stride 68 bf16), so every fragment read is one ds_read_b128 (K) or two ds_read_b64 (V);
+//   * Q (prescaled by scale·log2 e in f32) is split once into registers;
+//   * Sᵀ keeps the exact form's lane layout (query on the lane, keys 4(l >> 4) + r of each 16-key
+//     fragment), so the online softmax is unchanged; P is split per 32-key step, its k slots
+//     j < 4 / j ≥ 4 being keys 4(l >> 4) + j of the step's first / second fragment, and Vᵀ is read
+//     at exactly those keys.
+constexpr int KR3 = 64;  // bf16 per K plane row
+constexpr int VT3 = 68;  // bf16 per Vᵀ plane row (34 dwords)
+
+__global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
+  __shared__ __attribute__((aligned(16))) unsigned short kp[2][2][KT * KR3];  // [slot][hi, lo]
+  __shared__ __attribute__((aligned(16))) unsigned short vp[2][2][64 * VT3];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, qq = lane >> 4;
+  const int head = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * QBF + wid * QF * 16;
+  const float* Q = p.q + (long)b * p.q_bs + head * 64;
+  const float* Kg = p.k + (long)b * p.k_bs + head * 64;
+  const float* Vg = p.v + (long)b * p.v_bs + head * 64;
+
+  // Q fragments: step t holds Q[q0 + 16f + fr][32t + 8qq .. +7] · scale·log2(e), split
+  bf16x8 qh[QF][2], ql[QF][2];
+#pragma unroll
+  for (int f = 0; f < QF; ++f) {
+    const int qi = q0 + 16 * f + fr;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = {0.f, 0.f, 0.f, 0.f};
+      if (qi < p.Sq) {
+        x0 = *(const f32x4*)(Q + (long)qi * p.q_ld + 32 * t + 8 * qq) * p.sl2;
+        x1 = *(const f32x4*)(Q + (long)qi * p.q_ld + 32 * t + 8 * qq + 4) * p.sl2;
+      }
+      rdmi::split_bf16x8(x0, x1, qh[f][t], ql[f][t]);
+    }
+  }
+
+  f32x4 kr[LPT], vr[LPT];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = i * 64 * NWF + tid;
+      const int row = idx >> 4, ch = idx & 15;
+      const int key = kt * KT + row;
+      const bool ok = key < p.Sk;
+      kr[i] = ok ? *(const f32x4*)(Kg + (long)key * p.k_ld + ch * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      vr[i] = ok ? *(const f32x4*)(Vg + (long)key * p.v_ld + ch * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto lstore = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int idx = i * 64 * NWF + tid;
+      const int row = idx >> 4, ch = idx & 15;  // key row, d = 4ch .. 4ch+3
+      u32x2 s0 = rdmi::split_bf16x2(kr[i][0], kr[i][1]), s1 = rdmi::split_bf16x2(kr[i][2], kr[i][3]);
+      u32x2 h = {s0[0], s1[0]}, l = {s0[1], s1[1]};
+      const int ko = row * KR3 + (((ch >> 1) ^ (row & 7)) << 3) + (ch & 1) * 4;
+      *(u32x2*)&kp[slot][0][ko] = h;
+      *(u32x2*)&kp[slot][1][ko] = l;
+      s0 = rdmi::split_bf16x2(vr[i][0], vr[i][1]);
+      s1 = rdmi::split_bf16x2(vr[i][2], vr[i][3]);
+      h = u32x2{s0[0], s1[0]};
+      l = u32x2{s0[1], s1[1]};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int vo = (4 * ch + e) * VT3 + row;
+        vp[slot][0][vo] = (unsigned short)(h[e >> 1] >> (16 * (e & 1)));
+        vp[slot][1][vo] = (unsigned short)(l[e >> 1] >> (16 * (e & 1)));
+      }
+    }
+  };
+
+  f32x4 o[QF][4];  // Oᵀ fragments: d = 16e + 4qq + r, query = 16f + fr
+  float m[QF], l[QF];
+#pragma unroll
+  for (int f = 0; f < QF; ++f) {
+    m[f] = -INFINITY;
+    l[f] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[f][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int nkt = (p.Sk + KT - 1) / KT;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int slot = kt & 1;
+    if (kt + 1 < nkt) gload(kt + 1);
+    const unsigned short* kh = kp[slot][0];
+    const unsigned short* kl = kp[slot][1];
+    const unsigned short* vh = vp[slot][0];
+    const unsigned short* vl = vp[slot][1];
+    // Sᵀ = K·Qᵀ
+    f32x4 s[QF][KFR];
+#pragma unroll
+    for (int f = 0; f < QF; ++f)
+#pragma unroll
+      for (int g = 0; g < KFR; ++g) s[f][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < KFR; ++g) {
+      const int row = 16 * g + fr;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int off = row * KR3 + (((4 * t + qq) ^ (row & 7)) << 3);
+        const bf16x8 ah = *(const bf16x8*)(kh + off), al = *(const bf16x8*)(kl + off);
+#pragma unroll
+        for (int f = 0; f < QF; ++f) {
+          s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, qh[f][t], s[f][g], 0, 0, 0);
+          s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, qh[f][t], s[f][g], 0, 0, 0);
+          s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, ql[f][t], s[f][g], 0, 0, 0);
+        }
+      }
+    }
+    if ((kt + 1) * KT > p.Sk) {
+#pragma unroll
+      for (int g = 0; g < KFR; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * KT + 16 * g + 4 * qq + r >= p.Sk)
+#pragma unroll
+            for (int f = 0; f < QF; ++f) s[f][g][r] = -INFINITY;
+    }
+    // online softmax (exp2 domain), as the exact form
+#pragma unroll
+    for (int f = 0; f < QF; ++f) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < KFR; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[f][g][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[f], mx);
+      const float alpha = exp2f(m[f] - mn);
+      m[f] = mn;
+      float sum = 0.f;
+#pragma unroll
+      for (int g = 0; g < KFR; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = exp2f(s[f][g][r] - mn);
+          s[f][g][r] = pv;
+          sum += pv;
+        }
+      l[f] = l[f] * alpha + sum;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[f][e] *= alpha;
+    }
+    // Oᵀ += Vᵀ·Pᵀ in two 32-key steps
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      bf16x8 ph[QF], pl[QF];
+#pragma unroll
+      for (int f = 0; f < QF; ++f) rdmi::split_bf16x8(s[f][2 * u], s[f][2 * u + 1], ph[f], pl[f]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int vo = (16 * e + fr) * VT3 + 32 * u + 4 * qq;
+        const u32x2 h0 = *(const u32x2*)(vh + vo), h1 = *(const u32x2*)(vh + vo + 16);
+        const u32x2 l0 = *(const u32x2*)(vl + vo), l1 = *(const u32x2*)(vl + vo + 16);
+        const bf16x8 bh = __builtin_bit_cast(bf16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
+        const bf16x8 bl = __builtin_bit_cast(bf16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
+#pragma unroll
+        for (int f = 0; f < QF; ++f) {
+          o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ph[f], o[f][e], 0, 0, 0);
+          o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ph[f], o[f][e], 0, 0, 0);
+          o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, pl[f], o[f][e], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < nkt) {
+      lstore(slot ^ 1);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < QF; ++f) {
+    float lt = l[f];
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    const float inv = 1.0f / lt;
+    const int qi = q0 + 16 * f + fr;
+    if (qi < p.Sq) {
+      float* orow = p.o + (long)b * p.o_bs + (long)qi * p.o_ld + head * 64;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *(f32x4*)(orow + 16 * e + 4 * qq) = o[f][e] * inv;
+    }
+  }
+}
+
 }  // namespace
 
 namespace rdmi {
 
 int attention_fwd_f32(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, long q_ld,
                       long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs, long o_bs, float scale,
-                      void* stream) {
+                      bool x3, void* stream) {
   RDMI_REQUIRE(q_ld % 4 == 0 && k_ld % 4 == 0 && v_ld % 4 == 0 && o_ld % 4 == 0 &&
                    ((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) == 0),
                RDMI_E_ALIGN, "attention_fwd f32: strides/pointers must be 16-byte aligned");
   AttnF32P p{(const float*)q, (const float*)k, (const float*)v, (float*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld,
              q_bs, k_bs, v_bs, o_bs, scale * 1.4426950408889634f};
   dim3 g(rdmi::div_up(Sq, QBF), H, B);
+  if (x3) {
+    hipLaunchKernelGGL(attn_fwd_f32x3, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
+    return rdmi::check_launch("attention_fwd f32x3");
+  }
   hipLaunchKernelGGL(attn_fwd_f32, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
   return rdmi::check_launch("attention_fwd f32");
 }

@@ -17,6 +17,9 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
@@ -33,7 +36,7 @@ int conv2d_f32(const rdmi_conv_args* a, void* stream);
 // f32 flash attention behind rdmi_attention_fwd (attention_f32.hip)
 int attention_fwd_f32(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, long q_ld,
                       long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs, long o_bs, float scale,
-                      void* stream);
+                      bool x3, void* stream);
 
 inline int div_up(long a, long b) { return (int)((a + b - 1) / b); }
 
@@ -66,6 +69,25 @@ __device__ __forceinline__ void tile_mn(int logical, int nbx, int nby, int G, in
 template <int N>
 __device__ __forceinline__ void wait_vmcnt_only() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// Two f32 values → their packed bf16 hi and lo parts (v_cvt_pk_bf16_f32, first operand in the low
+// half; round-to-nearest-even both times): x = x_hi + x_lo + O(2^-18 |x|).  The f32 engines'
+// bf16-split products (rdmi.h RDMI_F32_X3) are built from these.
+__device__ __forceinline__ u32x2 split_bf16x2(float x0, float x1) {  // {hi, lo}
+  unsigned hi, lo;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(hi) : "v"(x0), "v"(x1));
+  const float r0 = x0 - __builtin_bit_cast(float, hi << 16), r1 = x1 - __builtin_bit_cast(float, hi & 0xffff0000u);
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(lo) : "v"(r0), "v"(r1));
+  return u32x2{hi, lo};
+}
+
+// 8 f32 values (a0 then a1) → bf16x8 hi and lo parts
+__device__ __forceinline__ void split_bf16x8(const f32x4& a0, const f32x4& a1, bf16x8& hi, bf16x8& lo) {
+  const u32x2 s0 = split_bf16x2(a0[0], a0[1]), s1 = split_bf16x2(a0[2], a0[3]);
+  const u32x2 s2 = split_bf16x2(a1[0], a1[1]), s3 = split_bf16x2(a1[2], a1[3]);
+  hi = __builtin_bit_cast(bf16x8, u32x4{s0[0], s1[0], s2[0], s3[0]});
+  lo = __builtin_bit_cast(bf16x8, u32x4{s0[1], s1[1], s2[1], s3[1]});
 }
 
 }  // namespace rdmi

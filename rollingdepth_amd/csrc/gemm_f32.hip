@@ -26,8 +26,6 @@
 // geometry of the f32 engine's K-tile, so the DMA and its swizzle are unchanged.
 #include "common.h"
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
 namespace {
 
 constexpr int BKF = 32;  // K per stage (floats)
@@ -136,22 +134,6 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
       }
     }
   }
-}
-
-// 8 f32 values → their bf16 hi and lo parts (round-to-nearest-even both times); x_hi + x_lo is x to
-// ≈2^-17 relative.  v_cvt_pk_bf16_f32 puts its first operand in the low half.
-__device__ __forceinline__ void split_bf16x8(const f32x4& a0, const f32x4& a1, bf16x8& hi, bf16x8& lo) {
-  const float x[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-  unsigned h[4], l[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(h[t]) : "v"(x[2 * t]), "v"(x[2 * t + 1]));
-    const float h0 = __builtin_bit_cast(float, h[t] << 16), h1 = __builtin_bit_cast(float, h[t] & 0xffff0000u);
-    const float r0 = x[2 * t] - h0, r1 = x[2 * t + 1] - h1;
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(l[t]) : "v"(r0), "v"(r1));
-  }
-  hi = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) unsigned){h[0], h[1], h[2], h[3]});
-  lo = __builtin_bit_cast(bf16x8, (__attribute__((ext_vector_type(4))) unsigned){l[0], l[1], l[2], l[3]});
 }
 
 // MODE 0: dense A [M, K]; MODE 1: implicit im2col of an NHWC f32 tensor for a 3×3 conv (any stride /
@@ -279,7 +261,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
         const int row = i * 16 + fr;
         const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ (row & 7)) << 2));
         const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ (row & 7)) << 2));
-        split_bf16x8(a0, a1, ah[i], al[i]);
+        rdmi::split_bf16x8(a0, a1, ah[i], al[i]);
       }
 #pragma unroll
       for (int j = 0; j < RN; ++j) {

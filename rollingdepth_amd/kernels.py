@@ -94,7 +94,8 @@ BF16 = torch.bfloat16
 
 
 def f32_x3() -> bool:
-    """Whether f32 weights are packed for the bf16-split engine (RDMI_F32_X3, rdmi.h; the default):
+    """Whether f32 weights are packed for the bf16-split engine (RDMI_F32_X3, rdmi.h; the default;
+    read when the weights are packed, and by attention() at each call for its own products):
     f32 activations and accumulation, three bf16 MFMA products per multiply-add (≈2^-16 relative per
     product, 2.2× the exact engine's speed on the paper preset's shapes: profiles/r03f_x3_probe.log).
     The reference's fp32 preset runs its convolutions through cuDNN with PyTorch's default
@@ -541,13 +542,16 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
     if out is None:
         out = torch.empty((B, Sq, HD), dtype=q.dtype, device=q.device)
     sc = 1.0 / math.sqrt(D) if scale is None else scale
-    name = "attention_fwd" if q.dtype == F16 else "attention_fwd_f32"
+    code = _dtype_code(q)
+    if code == _N.RDMI_F32 and f32_x3():
+        code = _N.RDMI_F32_X3  # bf16-split products (attention_f32.hip attn_fwd_f32x3)
+    name = {_N.RDMI_F16: "attention_fwd", _N.RDMI_F32: "attention_fwd_f32", _N.RDMI_F32_X3: "attention_fwd_f32x3"}[code]
     es = q.element_size()
     with _Timed(name, 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}",
                 es * B * heads * D * (2 * Sq + 2 * Sk)):
         check(lib.rdmi_attention_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), B, heads, Sq, Sk, D,
                                      q.stride(1), k.stride(1), v.stride(1), out.stride(1), q.stride(0), k.stride(0),
-                                     v.stride(0), out.stride(0), sc, _dtype_code(q), _stream()), "rdmi_attention_fwd")
+                                     v.stride(0), out.stride(0), sc, code, _stream()), "rdmi_attention_fwd")
     return out
 
 

@@ -80,3 +80,22 @@ for B, H, W, Cin, Cout, up in ((3, 96, 96, 320, 320, False), (3, 48, 48, 640, 64
     print(line, flush=True)
     del x, ref, xn
     torch.cuda.empty_cache()
+
+# cross-frame attention of the 768² snippet (3 frames): L0 S = 27648 (5 heads), L1 6912 (10), L2 1728 (20)
+for B, S, H in ((1, 27648, 5), (2, 6912, 10), (4, 1728, 20)):
+    C = H * 64
+    qkv = torch.randn(B, S, 3 * C, device=DEV, generator=g)
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    rows = torch.randint(0, S, (256,), device=DEV, generator=g)
+    qh = q.double()[:, rows].view(B, 256, H, 64).transpose(1, 2)
+    ref = F.scaled_dot_product_attention(qh, k.double().view(B, S, H, 64).transpose(1, 2),
+                                         v.double().view(B, S, H, 64).transpose(1, 2)).transpose(1, 2).reshape(B, 256, C)
+    line = f"attention B={B} S={S} H={H}:"
+    for x3 in ("0", "1"):
+        os.environ["RDMI_F32_X3"] = x3
+        o = K.attention(q, k, v, H)
+        ms = _time(lambda: K.attention(q, k, v, H, out=o), n=3)
+        tf = 4.0 * B * H * S * S * 64 / ms / 1e9
+        err = (o[:, rows].double() - ref).abs().max().item()
+        line += f" | {'x3' if x3 == '1' else 'f32'} {ms:.3f} ms {tf:.0f} TF/s max|Δ| {err:.1e}"
+    print(line, flush=True)
