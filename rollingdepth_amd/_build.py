@@ -3,7 +3,7 @@
     python -m rollingdepth_amd._build [--force]
 
 Each csrc/*.hip / *.cpp is compiled to an object under build/ (incremental on mtimes of the
-source, csrc/common.h and include/rdmi.h) and linked into rollingdepth_amd/_lib/librdmi.so, which
+source, the csrc/*.h headers and include/rdmi.h) and linked into rollingdepth_amd/_lib/librdmi.so, which
 travels to the GPU box with the repository snapshot.
 """
 from __future__ import annotations
@@ -30,8 +30,8 @@ def _sources():
 
 
 def _deps_mtime():
-    return max(os.path.getmtime(os.path.join(CSRC, "common.h")),
-               os.path.getmtime(os.path.join(ROOT, "include", "rdmi.h")))
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    return max(os.path.getmtime(h) for h in hdrs + [os.path.join(ROOT, "include", "rdmi.h")])
 
 
 def _compile(src, force):
