@@ -25,7 +25,18 @@ struct AttnP {
   int H, Sq, Sk;
   long q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs;
   float sl2;  // scale * log2(e)
+  unsigned long long* stamps;  // STAMP builds only (tools/attn_stamp.hip): per-wave segment cycle sums
 };
+
+// In-kernel stamp (diagnostic builds, STAMP = 1; guide §7 'In-kernel stamps'): s_memtime with the
+// lgkmcnt(0) it needs in one statement, fenced from the scheduler on both sides.
+__device__ __forceinline__ unsigned long long attn_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 constexpr int NWV = 8;        // waves per workgroup
 constexpr int QB = 32 * NWV;  // queries per workgroup (32 per wave)
@@ -72,8 +83,19 @@ constexpr int NSLOT = 5;
 // (MFMA block pinned by sched_barrier) or a static s_setprio 1 for waves 4-7 instead: within ±2 %
 // run-to-run (profiles/r01_attn_prio_ab.log); one row-sum partial per key block (4 independent
 // add chains instead of one) −11 %.
-template <bool F16SUM>
+// STAMP = 1 (diagnostic build only): per-wave cycle sums of the segments — 0 MFMA block, 1 its
+// barrier, 2 softmax block, 3 DMA wait + barrier, 4 prologue, 5 epilogue — written to p.stamps.
+template <bool F16SUM, int STAMP = 0>
 __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
+  unsigned long long st_acc[6] = {}, st_prev = 0;
+  auto seg = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long t = attn_stamp();
+      st_acc[i] += t - st_prev;
+      st_prev = t;
+    }
+  };
+  if constexpr (STAMP) st_prev = attn_stamp();
   __shared__ __attribute__((aligned(16))) f16 lds[NSLOT * 2 * TILE];  // 160 KB: slot s = [K | V]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -215,6 +237,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   __builtin_amdgcn_s_barrier();
   if (grp == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind group 0
   asm volatile("" ::: "memory");
+  seg(4);
 
   for (int kt = 0; kt < nt; ++kt) {
     // ================= M(kt): PV of the previous tile, S' of this tile.  The s_setprio pair keeps
@@ -234,9 +257,11 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
       }
     }
     __builtin_amdgcn_s_setprio(0);
+    seg(0);
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    seg(1);
     // ================= S(kt): softmax → P(kt); wait DMA(kt+2)
     issue(kt + 3);  // past the end: zero rows into a drained slot
     // ---- mask (last tile only; lane owns query c, keys (r&3)+8(r>>2)+4hh of each block)
@@ -293,10 +318,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
       if (F16SUM) rs = psum();
     }
     l += rs;
+    seg(2);
     attn_wait_vmcnt<2 * DPW>();  // DMA(kt+2) landed (DMA(kt+3) in flight)
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    seg(3);
   }
   // ================= M(nt): PV of the last tile
   pv((nt - 1) % NSLOT);
@@ -315,6 +342,13 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
         for (int e = 0; e < 4; ++e) w[e] = (f16)(o[d][4 * g + e] * inv);
         *(f16x4*)(O + d * 32 + 8 * g + 4 * hh) = w;
       }
+  }
+  if constexpr (STAMP) {
+    seg(5);
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + ((((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * NWV + wid) * 6;
+      for (int i = 0; i < 6; ++i) o[i] = st_acc[i];
+    }
   }
 }
 
@@ -591,7 +625,7 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
   RDMI_REQUIRE(q_ld % 8 == 0 && k_ld % 8 == 0 && v_ld % 8 == 0 && o_ld % 4 == 0 && (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) == 0,
                RDMI_E_ALIGN, "attention_fwd: strides/pointers must be 16-byte aligned");
   AttnP p{(const f16*)q, (const f16*)k, (const f16*)v, (f16*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs,
-          scale * 1.4426950408889634f};
+          scale * 1.4426950408889634f, nullptr};
   dim3 g(rdmi::div_up(Sq, QB), H, B);
   static const bool f32sum = [] { const char* e = getenv("RDMI_ATTN_F32SUM"); return e && e[0] == '1'; }();
   if (!f32sum)

@@ -10,6 +10,10 @@ if [ "${ISA:-0}" = "1" ]; then
   timeout -k 10 120 ./tools/isa_rate > gpurun_out/${TAG}_isa_rate.log 2>&1
   rc=$?; echo "isa_rate exit $rc"; if fatal $rc; then exit $rc; fi
 fi
+if [ -n "${AB:-}" ]; then  # AB="--env X --values a,b ..." : tools/conv_ab.py
+  timeout -k 10 ${AB_TIMEOUT:-300} python -u tools/conv_ab.py ${AB} > gpurun_out/${TAG}_conv_ab.log 2>&1
+  rc=$?; echo "conv_ab exit $rc"; if fatal $rc; then exit $rc; fi
+fi
 if [ -n "${TESTS:-}" ]; then
   timeout -k 10 ${TEST_TIMEOUT:-700} python -u -m pytest ${TESTS} -m gpu ${TESTK:+-k "$TESTK"} \
     --maxfail=${MAXFAIL:-10} -v -s --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.log 2>&1
