@@ -84,25 +84,47 @@ __device__ __forceinline__ int row_owner(const AlP& p, int r, int f, int& k_out)
   return -1;
 }
 
+// Block sums of NV doubles at once, each in block_sum_d's order (the xor butterfly inside a wave,
+// then the 4 wave partials in wave order): one LDS round instead of NV.  Result valid in thread 0.
+template <int NV>
+__device__ __forceinline__ void block_sums_d(double (&v)[NV]) {
+  __shared__ double sh[NV][4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += __shfl_xor(v[i], o, 64);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) sh[i][threadIdx.x >> 6] = v[i];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      double r = 0.0;
+      for (int w = 0; w < 4; ++w) r += sh[i][w];
+      v[i] = r;
+    }
+}
+
 // One (frame f, pixel chunk c) work unit of frame_stats; thread 0 returns the chunk's min/max of T.
 __device__ __forceinline__ void frame_stats_body(const AlP& p, int f, int c, float& mn_out, float& mx_out) {
-  __shared__ double sh[8];
-  // the slots covering frame f in row order (block-uniform): snippet row pointer, s, t
+  // the slots covering frame f in row order (block-uniform): snippet row pointer, s, t — one row
+  // per lane of wave 0 (R <= MAXR = 64), compacted in row order by a ballot
   __shared__ const float* ex[MAXR];
   __shared__ float es[MAXR], et[MAXR];
   __shared__ int ecnt;
-  if (threadIdx.x == 0) {
-    int cnt = 0;
-    for (int r = 0; r < p.R; ++r) {
-      int k = 0;
-      const int d = row_owner(p, r, f, k);
-      if (d < 0) continue;
-      ex[cnt] = p.x[d] + ((long)k * p.w[d] + (r - p.rb[d])) * p.P;
-      es[cnt] = p.s[d][k];
-      et[cnt] = p.t[d][k];
-      ++cnt;
+  if (threadIdx.x < 64) {
+    const int r = threadIdx.x;
+    int k = 0;
+    const int d = r < p.R ? row_owner(p, r, f, k) : -1;
+    const unsigned long long m = __ballot(d >= 0);
+    if (d >= 0) {
+      const int slot = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      ex[slot] = p.x[d] + ((long)k * p.w[d] + (r - p.rb[d])) * p.P;
+      es[slot] = p.s[d][k];
+      et[slot] = p.t[d][k];
     }
-    ecnt = cnt;
+    if (r == 0) ecnt = __popcll(m);
   }
   __syncthreads();
   const int cnt = ecnt;
@@ -129,8 +151,6 @@ __device__ __forceinline__ void frame_stats_body(const AlP& p, int f, int c, flo
     mn = fminf(mn, T);
     mx = fmaxf(mx, T);
   }
-  double A = block_sum_d<256>(sa, sh);
-  double D = block_sum_d<256>(sd, sh);
   mn = wave_min(mn);
   mx = wave_max(mx);
   __shared__ float r[2][4];
@@ -138,11 +158,12 @@ __device__ __forceinline__ void frame_stats_body(const AlP& p, int f, int c, flo
     r[0][threadIdx.x >> 6] = mn;
     r[1][threadIdx.x >> 6] = mx;
   }
-  __syncthreads();
+  double v[2] = {sa, sd};
+  block_sums_d<2>(v);  // its barrier also publishes r
   if (threadIdx.x == 0) {
     double* o = p.fpart + ((long)f * PS + c) * 4;
-    o[0] = A;
-    o[1] = D;
+    o[0] = v[0];
+    o[1] = v[1];
     mn_out = fminf(fminf(r[0][0], r[0][1]), fminf(r[0][2], r[0][3]));
     mx_out = fmaxf(fmaxf(r[1][0], r[1][1]), fmaxf(r[1][2], r[1][3]));
   }
@@ -208,11 +229,9 @@ __device__ __forceinline__ void snippet_grad_body(const AlP& p, int gk, int c, d
       l2 += fabs((double)zd) * (double)iscd;
     }
   }
-  __shared__ double sh[8];
-  gs = block_sum_d<256>(gs, sh);
-  gt = block_sum_d<256>(gt, sh);
-  l1 = block_sum_d<256>(l1, sh);
-  l2 = block_sum_d<256>(l2, sh);
+  double v[4] = {gs, gt, l1, l2};
+  block_sums_d<4>(v);
+  gs = v[0], gt = v[1], l1 = v[2], l2 = v[3];
   if (threadIdx.x == 0) {
     const long o = (long)gk * PS + c;
     if (COHERENT) {

@@ -397,6 +397,10 @@ def main():
     if "full1024" in todo:  # full preset: 1024², [1,10,25] capped as the reference caps, refine 10
         compact_fixture(P, "full1024", C.SD2_UNET, C.SD2_VAE, 6, 1024, [1, 10, 25], True, 4, refine_step=10,
                         refine_start=6)
+    if "full1024_mix" in todo:  # full preset at 1024² on 12 frames: [1,10,25] capped to [1,3,3] by the
+        # reference (max gap int(12/3)-1 = 3), so two distinct dilations are co-aligned and refined
+        compact_fixture(P, "full1024_mix", C.SD2_UNET, C.SD2_VAE, 12, 1024, [1, 10, 25], True, 4, refine_step=10,
+                        refine_start=6)
     if "paper256" in todo:  # paper preset semantics (fp32, cap_dilation False, refine 10) at 256², N=51
         compact_fixture(P, "paper256", C.SD2_UNET, C.SD2_VAE, 51, 256, [1, 10, 25], False, 2, refine_step=10,
                         refine_start=6)
