@@ -16,6 +16,8 @@
 //   run as GEMM → softmax → GEMM.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -352,6 +354,329 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   }
 }
 
+// attn_fwd_d64_pipe: the same arithmetic as attn_fwd_d64, restructured for ONE wave per SIMD.
+//
+// Why (tools/attn_stamp.hip, profiles/r03h_attn_stamp.log): in attn_fwd_d64 the two waves of a SIMD
+// alternate an MFMA block (32 MFMAs = 1 024 matrix cycles) with a softmax block, and both blocks
+// measure ≈1 500 cycles per 128-key tile: the SIMD's one vector-issue port serves the softmax wave's
+// ≈850 issue cycles of exp / cvt / add AND the MFMA wave's issue holds (8 of every 32 cycles), so
+// the matrix pipe idles ≈35 % of the time.  Here each wave owns its SIMD and interleaves its own
+// softmax with its own MFMAs (software pipeline; guide §5.5 T15, Appendix B 'Fused attention
+// prefill', 4-wave structure).  A wave holds 64 queries as two 32-query blocks q0, q1 that share
+// every K and V fragment; per 32-key sub-tile u the MFMA stream is
+//     PV_q0(u) | QK_q0(u+1) | PV_q1(u) | QK_q1(u+1)        (4 MFMAs each)
+// and the softmax of S_q1(u) runs beside the first two segments, that of S_q0(u+1) beside the last
+// two, each followed by its block's m̃ / rescale decision — so every 32-cycle MFMA gap carries ≈4
+// vector instructions (2 exponentials), and only one 16-register S per block is live.  A workgroup
+// = 4 waves = 256 queries; K/V in 64-key tiles by LDS-DMA into a 4-slot ring, one barrier per tile.
+// Same exponent / rounding order per query as attn_fwd_d64; the packed-f16 row sum is taken per 32
+// keys instead of per 64 (results equal to f16 rounding of P sums).
+namespace pp {
+constexpr int NW = 4;              // waves per workgroup (one per SIMD)
+constexpr int QB = 64 * NW;        // queries per workgroup (64 per wave)
+constexpr int TK = 64;             // keys per K/V tile (DMA and barrier granule): 2 sub-tiles of 32
+constexpr int NSL = 4;             // tile slots in the LDS ring
+constexpr int TH = TK * 64;        // halves per K (or V) tile (8 KiB)
+constexpr int DPW = TK / 8 / NW;   // 8-row DMA pieces per wave per tile per tensor (2)
+}  // namespace pp
+
+template <int STAMP = 0>
+__global__ __launch_bounds__(64 * pp::NW, 2) void attn_fwd_d64_pipe(AttnP p) {
+  constexpr int NW = pp::NW, QB = pp::QB, TK = pp::TK, NSL = pp::NSL, TH = pp::TH, DPW = pp::DPW;
+  __shared__ __attribute__((aligned(16))) f16 lds[NSL * 2 * TH];  // 64 KiB: slot s = [K | V]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int hh = lane >> 5;
+  const int c = lane & 31;
+  const int head = blockIdx.y;
+  const int b = blockIdx.z;
+  const int q0 = blockIdx.x * QB + wid * 64;  // query block qb of this wave: q0 + 32 qb + c
+
+  const f16* Q = p.q + (long)b * p.q_bs + head * 64;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.k + (long)b * p.k_bs + head * 64), (short)0, (int)(((long)(p.Sk - 1) * p.k_ld + 64) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.v + (long)b * p.v_bs + head * 64), (short)0, (int)(((long)(p.Sk - 1) * p.v_ld + 64) * 2), 0x00020000);
+
+  // Q·scale·log2(e) as the B operand of Sᵀ = K·Qᵀ (rounded to f16 once), per query block
+  f16x8 qf[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qi = q0 + 32 * qb + c;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      f16x8 z = {};
+      const f16x8 qr = qi < p.Sq ? *(const f16x8*)(Q + (long)qi * p.q_ld + ks * 16 + hh * 8) : z;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[qb][ks][e] = (f16)((float)qr[e] * p.sl2);
+    }
+  }
+
+  // DMA lane geometry (as attn_fwd_d64): row = (i·NW + wid)·8 + drow of the 64-key tile
+  const int drow = lane >> 3;
+  unsigned koff[DPW], voff[DPW];
+#pragma unroll
+  for (int i = 0; i < DPW; ++i) {
+    const int row = (i * NW + wid) * 8 + drow;
+    const int kchunk = (lane & 7) ^ ((row >> 1) & 7);
+    const int vchunk = (lane & 7) ^ (((row >> 1) & 1) << 2);
+    koff[i] = (unsigned)(row * p.k_ld + kchunk * 8) * 2u;
+    voff[i] = (unsigned)(row * p.v_ld + vchunk * 8) * 2u;
+  }
+  const unsigned kstep = (unsigned)(TK * p.k_ld * 2), vstep = (unsigned)(TK * p.v_ld * 2);
+  auto issue = [&](int kt) __attribute__((always_inline)) {  // past the end: zero rows (descriptor range)
+    const int slot = kt % NSL;
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      f16* ks_ = lds + slot * 2 * TH + (i * NW + wid) * 8 * 64;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)ks_, 16,
+                                               koff[i] + (unsigned)kt * kstep, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(ks_ + TH), 16,
+                                               voff[i] + (unsigned)kt * vstep, 0, 0, 0);
+    }
+  };
+
+  // fragment addresses (bytes): K row c of a 32-key sub-tile, chunk 2ks + hh swizzled by
+  // (row >> 1) & 7 = (c >> 1) & 7 (sub-tile row offsets are multiples of 16); Vᵀ by transposed
+  // reads of rows 16st + tr_key (+8), chunk swizzle (tr_key >> 1) & 1 — immediates per sub-tile
+  const unsigned lbase = (unsigned)(uintptr_t)LDS_PTR(f16, lds);
+  unsigned kaddr[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kaddr[ks] = (unsigned)((c * 64 + (((2 * ks + hh) ^ ((c >> 1) & 7)) << 3)) * 2);
+  const int gi = lane >> 4, li = lane & 15;
+  const int tr_key = 4 * (gi >> 1) + (li >> 2);
+  const int tr_col = 16 * (gi & 1) + 4 * (li & 3);
+  unsigned vaddr[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int col = d * 32 + tr_col;
+    const int pc = ((col >> 3) ^ (((tr_key >> 1) & 1) << 2)) << 3 | (col & 7);
+    vaddr[d] = (unsigned)((TH + tr_key * 64 + pc) * 2);
+  }
+  auto sub_base = [&](int u) __attribute__((always_inline)) {
+    return lbase + (unsigned)(((u >> 1) % NSL) * 2 * TH * 2 + (u & 1) * 32 * 64 * 2);
+  };
+
+  const int nt = (p.Sk + TK - 1) / TK;
+  const int nsub = (p.Sk + 31) / 32;  // sub-tiles holding keys
+
+  f32x16 o[2][2];  // [qb][d-block]: Oᵀ accumulators
+  // −m̃ enters the QKᵀ chain as a fifth k-step K' = [1 0 …], Q' = [−m̃ 0 …] (m̃ is an f16 value, so the
+  // product is exact), issued FIRST on a zero accumulator: the chain then starts from exactly −m̃ in
+  // every entry, as attn_fwd_d64's initial accumulator does, without 16 live registers per block
+  // (and without the copies of them into each chain's accumulator)
+  f16x8 kone = {}, qm[2] = {};
+  if (hh == 0) kone[0] = (f16)1.0f;
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[qb][d][r] = 0.f;
+  }
+  float mt[2] = {0.f, 0.f}, l[2] = {0.f, 0.f};
+  f16x8 kf[4];         // K fragments of the next sub-tile (shared by both blocks)
+  i16x4 vr[2][2][2];   // Vᵀ fragments of the current sub-tile [st][d][lo/hi] (shared by both blocks)
+  f32x16 s[2];         // S' of each block's current sub-tile
+  f16x8 pf[2][2];      // P of each block's current sub-tile [qb][16-key step]
+  float e[16];         // exponentials of the block being normalised
+
+  // Vᵀ reads as asm (hipcc drains the in-flight LDS-DMA, vmcnt(0), in front of a ds_read_tr builtin),
+  // counted by hand; K reads as plain loads, whose lgkmcnt hipcc places before each consumer (its
+  // counts ignore the asm reads issued before them, so they over-wait, never under-wait).  The V
+  // reads carry a "memory" clobber so the K loads stay behind them: lgkmcnt(4) then means "V landed".
+  auto kread = [&](int u) __attribute__((always_inline)) {
+    const f16* kb = lds + ((u >> 1) % NSL) * 2 * TH + (u & 1) * 32 * 64;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) kf[ks] = *(const f16x8*)(kb + kaddr[ks] / 2);
+  };
+  auto vread = [&](int u) __attribute__((always_inline)) {
+    const unsigned vb = sub_base(u);
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+                     : "=v"(vr[st][d][0]) : "v"(vb + vaddr[d]), "i"(st * 16 * 64 * 2) : "memory");
+        asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+                     : "=v"(vr[st][d][1]) : "v"(vb + vaddr[d]), "i"((st * 16 + 8) * 64 * 2) : "memory");
+      }
+  };
+  // the destinations count as written at the wait (guide §5.7 item 1 form ii)
+  auto vwait = [&](bool k_behind) __attribute__((always_inline)) {
+    if (k_behind)
+      asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(vr[0][0][0]), "+v"(vr[0][0][1]), "+v"(vr[0][1][0]), "+v"(vr[0][1][1]), "+v"(vr[1][0][0]),
+                 "+v"(vr[1][0][1]), "+v"(vr[1][1][0]), "+v"(vr[1][1][1]));
+  };
+  // S'_qb = K·Qᵀ − m̃ (five chained MFMAs, the −m̃ step first)
+  auto qk = [&](int qb) __attribute__((always_inline)) {
+    const f32x16 zero = {};
+    s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kone, qm[qb], zero, 0, 0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[ks], qf[qb][ks], s[qb], 0, 0, 0);
+  };
+  // Oᵀ_qb += Vᵀ·P_qbᵀ (two 16-key steps × two 32-row d-blocks)
+  auto pv = [&](int qb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const f16x8 vf =
+            __builtin_bit_cast(f16x8, __builtin_shufflevector(vr[st][d][0], vr[st][d][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        o[qb][d] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[qb][st], o[qb][d], 0, 0, 0);
+      }
+  };
+  // keys past Sk masked (guarded form: the sub-tile straddling the end)
+  auto mask = [&](int qb, int u, bool guarded) __attribute__((always_inline)) {
+    if (guarded && 32 * u + 32 > p.Sk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (32 * u + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.Sk) s[qb][r] = -INFINITY;
+    }
+  };
+  auto exps = [&](int qb, int lo, int hi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = lo; r < hi; ++r) e[r] = __builtin_amdgcn_exp2f(s[qb][r]);  // v_exp_f32, no denorm fixup
+  };
+  // f16 P (the PV B operand) and its packed-f16 row sum over this lane's 16 keys
+  auto pack_sum = [&](int qb) __attribute__((always_inline)) -> float {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pf[qb][r >> 3][r & 7] = (f16)e[r];
+    const f16x8 a = pf[qb][0] + pf[qb][1];
+    const f16x4 b4 = __builtin_shufflevector(a, a, 0, 1, 2, 3) + __builtin_shufflevector(a, a, 4, 5, 6, 7);
+    const f16x2 c2 = __builtin_shufflevector(b4, b4, 0, 1) + __builtin_shufflevector(b4, b4, 2, 3);
+    return (float)c2[0] + (float)c2[1];
+  };
+  // block qb's m̃: set on the first sub-tile, re-set (O_qb, l_qb rescaled, P recomputed) when its P
+  // would leave the f16 range.  O_qb holds PV of sub-tiles < u only; QK_qb(u+1) is issued after.
+  auto decide = [&](int qb, float rs, bool first) __attribute__((always_inline)) {
+    if (__builtin_expect(first || __any(!(rs <= 32768.f)), 0)) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[qb][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (!first) mx = fmaxf(mx, 0.f);            // never lower m̃ (l >= 1 stays true)
+      const float mnew = (float)(f16)(mt[qb] + mx);  // next m̃, an f16 value
+      const float delta = mnew - mt[qb];            // exact: both are f16 values
+      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
+      l[qb] *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[qb][d][r] *= alpha;
+      mt[qb] = mnew;
+      if (hh == 0) qm[qb][0] = (f16)(-mnew);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[qb][r] -= delta;
+      exps(qb, 0, 16);
+      rs = pack_sum(qb);
+    }
+    l[qb] += rs;
+  };
+
+  // prologue: DMA(0..2); tiles 0 and 1 landed; S'_q0(0), S'_q1(0); softmax + m̃ of block 0
+  issue(0);
+  issue(1);
+  issue(2);
+  attn_wait_vmcnt<2 * DPW>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  kread(0);
+  qk(0);
+  qk(1);
+  mask(0, 0, true);
+  exps(0, 0, 16);
+  decide(0, pack_sum(0), true);
+
+  // period u, two halves, each one basic block in the steady state:
+  //   A: [V(u), K(u+1) reads; 8 exps of S'_q1(u)] | PV_q0(u), QK_q0(u+1) ∥ the rest of softmax_q1(u)
+  //   decide q1
+  //   B: PV_q1(u), QK_q1(u+1) ∥ softmax_q0(u+1)
+  //   decide q0
+  // Tile barrier at the head of odd periods, before K of sub-tile u+1 (tile kt+1) is read: tile kt+1
+  // landed for every wave, and the slot of tile kt-1 (read for the last time in period u-2) free for
+  // DMA(kt+3).  Issue order inside each half pinned by sched_group_barrier (MFMA 0x8, VALU 0x2).
+  auto period = [&](int u, auto guarded, auto parity) __attribute__((always_inline)) {
+    constexpr bool G = decltype(guarded)::value;
+    constexpr int PAR = decltype(parity)::value;  // 0 / 1: u's parity known; 2: read from u
+    const bool nx = !G || u + 1 < nsub;
+    if (PAR == 1 || (PAR == 2 && (u & 1))) {
+      attn_wait_vmcnt<2 * DPW>();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue((u >> 1) + 3);
+    }
+    vread(u);
+    if (nx) kread(u + 1);
+    mask(1, u, G);
+    exps(1, 0, 8);
+    __builtin_amdgcn_sched_barrier(0);
+    vwait(nx);
+    pv(0);
+    exps(1, 8, 16);
+    if (nx) qk(0);
+    const float rs1 = pack_sum(1);
+    if constexpr (!G) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+    }
+    decide(1, rs1, G && u == 0);
+    pv(1);
+    if (nx) {
+      qk(1);
+      mask(0, u + 1, G);
+      exps(0, 0, 16);
+      const float rs0 = pack_sum(0);
+      if constexpr (!G) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+      }
+      decide(0, rs0, false);
+    }
+  };
+  // steady state while sub-tile u+1 is whole; the guarded form for the first two and the last sub-tiles
+  const int nst = p.Sk / 32 - 1;
+  int u = 0;
+  for (; u < 2 && u < nsub; ++u) period(u, std::true_type{}, std::integral_constant<int, 2>{});  // first of q1
+  for (; u + 1 < nst; u += 2) {
+    period(u, std::false_type{}, std::integral_constant<int, 0>{});
+    period(u + 1, std::false_type{}, std::integral_constant<int, 1>{});
+  }
+  for (; u < nsub; ++u) period(u, std::true_type{}, std::integral_constant<int, 2>{});
+  attn_wait_vmcnt<0>();  // drain trailing zero-row DMAs before the workgroup retires
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qi = q0 + 32 * qb + c;
+    const float lt = l[qb] + __shfl_xor(l[qb], 32, 64);
+    const float inv = 1.f / lt;
+    if (qi < p.Sq) {
+      f16* O = p.o + (long)b * p.o_bs + (long)qi * p.o_ld + head * 64;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = (f16)(o[qb][d][4 * g + e] * inv);
+          *(f16x4*)(O + d * 32 + 8 * g + 4 * hh) = w;
+        }
+    }
+  }
+}
+
 // one thread per (token, head); D == 64, L ≤ 16
 template <typename T>
 __global__ __launch_bounds__(256) void attn_smallkv(const T* __restrict__ q, const T* __restrict__ k,
@@ -628,6 +953,12 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
           scale * 1.4426950408889634f, nullptr};
   dim3 g(rdmi::div_up(Sq, QB), H, B);
   static const bool f32sum = [] { const char* e = getenv("RDMI_ATTN_F32SUM"); return e && e[0] == '1'; }();
+  const char* pe = getenv("RDMI_ATTN_PIPE");  // read per launch (A/B): 1 = the one-wave-per-SIMD pipeline
+  if (pe && pe[0] == '1' && !f32sum) {
+    hipLaunchKernelGGL(attn_fwd_d64_pipe<0>, dim3(rdmi::div_up(Sq, pp::QB), H, B), dim3(64 * pp::NW), 0,
+                       (hipStream_t)stream, p);
+    return rdmi::check_launch("attention_fwd");
+  }
   if (!f32sum)
     hipLaunchKernelGGL(attn_fwd_d64<true>, g, dim3(64 * NWV), 0, (hipStream_t)stream, p);
   else

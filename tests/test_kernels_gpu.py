@@ -384,8 +384,18 @@ def _sdpa_ref(q, k, v, heads):
     return o.transpose(1, 2).reshape(B, Sq, HD)
 
 
-@pytest.mark.parametrize("B,S,H", [(1, 192, 2), (2, 768, 5), (1, 432, 20), (3, 100, 1), (1, 3072, 5), (2, 65, 3)])
-def test_attention_fused_qkv(B, S, H):
+@pytest.fixture(params=["d64", "pipe"])
+def attn_engine(request, monkeypatch):
+    """Both head-dim-64 flash kernels: attn_fwd_d64 (two waves per SIMD, MFMA block ∥ softmax block;
+    the default) and attn_fwd_d64_pipe (RDMI_ATTN_PIPE=1: each wave interleaves its own softmax with
+    its MFMAs)."""
+    monkeypatch.setenv("RDMI_ATTN_PIPE", "1" if request.param == "pipe" else "0")
+    return request.param
+
+
+@pytest.mark.parametrize("B,S,H", [(1, 192, 2), (2, 768, 5), (1, 432, 20), (3, 100, 1), (1, 3072, 5), (2, 65, 3),
+                                   (1, 31, 2), (2, 1000, 1)])
+def test_attention_fused_qkv(B, S, H, attn_engine):
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(7)
     C = H * 64
@@ -397,7 +407,7 @@ def test_attention_fused_qkv(B, S, H):
 
 
 @pytest.mark.parametrize("B,S,H", [(2, 27648, 5), (1, 49152, 5)])
-def test_attention_pipeline_sizes_sampled_rows(B, S, H):
+def test_attention_pipeline_sizes_sampled_rows(B, S, H, attn_engine):
     """Level-0 cross-frame attention at the metric config (768²: S = 3·96² = 27 648, H = 5) and at
     1024² (S = 3·128² = 49 152), QKV as the fused projection writes it, against fp32 SDPA over all
     keys for 512 sampled query rows per snippet (the full fp32 reference would need S² scores)."""
@@ -415,7 +425,7 @@ def test_attention_pipeline_sizes_sampled_rows(B, S, H):
     assert err.max().item() < 5e-3 and err.mean().item() < 5e-4
 
 
-def test_attention_softmax_rescale_branch():
+def test_attention_softmax_rescale_branch(attn_engine):
     """A key spike late in the sequence forces the running-max rescale (guide rule 26)."""
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(8)
@@ -431,7 +441,7 @@ def test_attention_softmax_rescale_branch():
 
 
 @pytest.mark.parametrize("qscale,S", [(6.0, 700), (0.02, 300), (-4.0, 1000)])
-def test_attention_large_and_tiny_scores(qscale, S):
+def test_attention_large_and_tiny_scores(qscale, S, attn_engine):
     """Score ranges far outside the first tile's max (|scores| up to ~±60 in log2 units: the m̃
     re-set path fires on many tiles) and nearly uniform softmax (scores ≈ 0)."""
     K_ = _k()
@@ -448,7 +458,7 @@ def test_attention_large_and_tiny_scores(qscale, S):
     assert (o.float() - ref).abs().max().item() < (8e-3 if abs(qscale) > 1 else 5e-3)
 
 
-def test_attention_growing_max():
+def test_attention_growing_max(attn_engine):
     """Key norms grow along the sequence so the row max rises by a few units per tile: the m̃
     re-set (and O/l rescale) fires repeatedly at moderate jumps, never at the first tile only."""
     K_ = _k()

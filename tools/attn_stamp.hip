@@ -70,6 +70,41 @@ int main(int argc, char** argv) {
     }
     printf("%s build: %.3f ms  %.1f TF/s (B=%d H=%d S=%d)\n", variant ? "STAMP" : "plain", best, fl / best / 1e9, B, H, S);
   }
+  // the one-wave-per-SIMD pipeline (attn_fwd_d64_pipe): timing and max |Δ| against attn_fwd_d64
+  {
+    f16* o2;
+    CK(hipMalloc(&o2, n * 2));
+    AttnP p2 = p;
+    p2.o = o2;
+    dim3 g2(rdmi::div_up(S, pp::QB), H, B);
+    // extra dynamic LDS forces one workgroup per CU (one wave per SIMD) for the A/B
+    const size_t xl = getenv("PIPE_1WG") ? 80 * 1024 : 0;
+    float best = 1e30f;
+    for (int r = 0; r < 6; ++r) {
+      CK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL((attn_fwd_d64_pipe<0>), g2, dim3(64 * pp::NW), xl, 0, p2);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    hipLaunchKernelGGL((attn_fwd_d64<true, 0>), g, dim3(64 * NWV), 0, 0, p);
+    CK(hipDeviceSynchronize());
+    std::vector<f16> a(n), c2(n);
+    CK(hipMemcpy(a.data(), o, n * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(c2.data(), o2, n * 2, hipMemcpyDeviceToHost));
+    double md = 0, ma = 0;
+    long bad = 0;
+    for (long i = 0; i < n; ++i) {
+      const double x = (double)(float)a[i], y = (double)(float)c2[i];
+      if (!(y == y)) ++bad;
+      md = fmax(md, fabs(x - y));
+      ma = fmax(ma, fabs(x));
+    }
+    printf("pipe%s build: %.3f ms  %.1f TF/s   max |pipe - d64| %.3e (max |O| %.3f, non-finite %ld)\n", xl ? "(1wg)" : "", best,
+           fl / best / 1e9, md, ma, bad);
+  }
   std::vector<unsigned long long> h(nw * 6);
   CK(hipMemcpy(h.data(), st, nw * 6 * 8, hipMemcpyDeviceToHost));
   const char* names[6] = {"MFMA block (PV t-1, QK t)", "barrier after MFMA block", "softmax block", "DMA wait + barrier",
