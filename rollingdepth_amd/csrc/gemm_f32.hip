@@ -139,14 +139,16 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
 // MODE 0: dense A [M, K]; MODE 1: implicit im2col of an NHWC f32 tensor for a 3×3 conv (any stride /
 // padding, K order [tap][Cin]); MODE 2: the 3×3 conv reading x through a nearest ×2 upsample.
 // X3: bf16-split products (header).
-template <int MODE, bool X3>
-__global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
+// NS: LDS ring slots — 3 (96 KiB: one workgroup per CU, two K-tiles in flight) or 2 (64 KiB: two
+// workgroups per CU, one K-tile in flight; the co-resident workgroup covers the DMA latency).
+template <int MODE, bool X3, int NS>
+__global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P p) {
   constexpr int BM = 128, BN = 128, NW = 4, WTM = 64, WTN = 64;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int AV = BM / 8 / NW, BV = BN / 8 / NW;  // 1-KiB DMA instructions per wave per K-tile
   constexpr int LPS = AV + BV;
   constexpr int SLOT = (BM + BN) * BKF;  // floats
-  __shared__ __attribute__((aligned(16))) float lds[3 * SLOT];  // 96 KiB
+  __shared__ __attribute__((aligned(16))) float lds[NS * SLOT];  // 96 / 64 KiB
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -242,16 +244,19 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32P p) {
 
   const int nk = (p.K + BKF - 1) / BKF;
   issue(0, 0);
-  issue(1, 1);
+  if (NS == 3) issue(1, 1);
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    rdmi::wait_vmcnt_only<LPS>();
+    if (NS == 3)
+      rdmi::wait_vmcnt_only<LPS>();  // K-tile kt landed (kt+1 in flight)
+    else
+      rdmi::wait_vmcnt_only<0>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    issue(kt + 2, (kt + 2) % 3);
-    const float* la = lds + (kt % 3) * SLOT + (wm * WTM) * BKF;
-    const float* lb = lds + (kt % 3) * SLOT + BM * BKF + (wn * WTN) * BKF;
+    issue(kt + NS - 1, (kt + NS - 1) % NS);  // into the slot read last in K-tile kt-1
+    const float* la = lds + (kt % NS) * SLOT + (wm * WTM) * BKF;
+    const float* lb = lds + (kt % NS) * SLOT + BM * BKF + (wn * WTN) * BKF;
     if constexpr (X3) {
       // lane quarter fq holds k = 8fq .. 8fq+7 of its row in both operands (the bf16 16x16x32 layout):
       // A as f32 chunks 2fq, 2fq+1 (split here), W as bf16 chunks fq (hi) and 4+fq (lo)
@@ -320,11 +325,20 @@ int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode, bool x3) {
   const char* gm = getenv("RDMI_GEMM_GROUP");
   p.group_m = gm ? atoi(gm) : 8;
   dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
+  // RDMI_F32_SLOTS (read per launch, A/B): unset / 2 = two workgroups per CU with a 2-slot ring (the
+  // default: +30-40 % for the bf16-split products, +12-15 % exact, bitwise the same —
+  // profiles/r03k_f32_slots_ab.log), 3 = one workgroup per CU with a 3-slot ring
+  const char* se = getenv("RDMI_F32_SLOTS");
+  const bool ns2 = !(se && se[0] == '3');
 #define RDMI_F32_LAUNCH(M)                                                                     \
-  if (x3)                                                                                      \
-    hipLaunchKernelGGL((gemm_f32_kernel<M, true>), g, dim3(256), 0, s, p);                    \
+  if (x3 && ns2)                                                                               \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, true, 2>), g, dim3(256), 0, s, p);                 \
+  else if (x3)                                                                                 \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, true, 3>), g, dim3(256), 0, s, p);                 \
+  else if (ns2)                                                                                \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, false, 2>), g, dim3(256), 0, s, p);                \
   else                                                                                         \
-    hipLaunchKernelGGL((gemm_f32_kernel<M, false>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<M, false, 3>), g, dim3(256), 0, s, p);
   if (mode == 2) {
     RDMI_F32_LAUNCH(2)
   } else if (mode == 1) {
