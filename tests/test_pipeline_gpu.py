@@ -201,6 +201,13 @@ def test_full1024_refine_vs_reference_golden():
     _run_compact("full1024")
 
 
+def test_full1024_mixed_dilations_vs_reference_golden():
+    """full preset at 1024² on 12 frames: the reference caps [1, 10, 25] to [1, 3, 3], so two distinct
+    dilations are co-aligned and refined at the full preset's resolution (full1024's 6 frames collapse
+    to [1, 1, 1])."""
+    _run_compact("full1024_mix")
+
+
 def test_paper256_f16_vs_reference_golden():
     """Paper preset shape (dilations [1, 10, 25] uncapped, refine 10) on 51 frames at 256², f16 path
     against the reference's fp32 run."""
