@@ -237,12 +237,15 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
     }
   }
 
+  // staging geometry: thread tid moves key rows 2(tid >> 4) + i (i < LPT = 2), head dims 4ch .. 4ch+3
+  // (ch = tid & 15: 16 threads per 256-B row), so the Vᵀ planes take the two keys of a d as one
+  // 32-bit store
+  static_assert(LPT == 2, "two key rows per thread");
   f32x4 kr[LPT], vr[LPT];
   auto gload = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int idx = i * 64 * NWF + tid;
-      const int row = idx >> 4, ch = idx & 15;
+      const int row = 2 * (tid >> 4) + i, ch = tid & 15;
       const int key = kt * KT + row;
       const bool ok = key < p.Sk;
       kr[i] = ok ? *(const f32x4*)(Kg + (long)key * p.k_ld + ch * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -250,25 +253,26 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
     }
   };
   auto lstore = [&](int slot) {
+    const int ch = tid & 15, row0 = 2 * (tid >> 4);
+    u32x2 vh[LPT], vl[LPT];
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int idx = i * 64 * NWF + tid;
-      const int row = idx >> 4, ch = idx & 15;  // key row, d = 4ch .. 4ch+3
+      const int row = row0 + i;  // key row, d = 4ch .. 4ch+3
       u32x2 s0 = rdmi::split_bf16x2(kr[i][0], kr[i][1]), s1 = rdmi::split_bf16x2(kr[i][2], kr[i][3]);
-      u32x2 h = {s0[0], s1[0]}, l = {s0[1], s1[1]};
       const int ko = row * KR3 + (((ch >> 1) ^ (row & 7)) << 3) + (ch & 1) * 4;
-      *(u32x2*)&kp[slot][0][ko] = h;
-      *(u32x2*)&kp[slot][1][ko] = l;
+      *(u32x2*)&kp[slot][0][ko] = u32x2{s0[0], s1[0]};
+      *(u32x2*)&kp[slot][1][ko] = u32x2{s0[1], s1[1]};
       s0 = rdmi::split_bf16x2(vr[i][0], vr[i][1]);
       s1 = rdmi::split_bf16x2(vr[i][2], vr[i][3]);
-      h = u32x2{s0[0], s1[0]};
-      l = u32x2{s0[1], s1[1]};
+      vh[i] = u32x2{s0[0], s1[0]};  // d 4ch..4ch+3 of key row0 + i, bf16 pairs
+      vl[i] = u32x2{s0[1], s1[1]};
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int vo = (4 * ch + e) * VT3 + row;
-        vp[slot][0][vo] = (unsigned short)(h[e >> 1] >> (16 * (e & 1)));
-        vp[slot][1][vo] = (unsigned short)(l[e >> 1] >> (16 * (e & 1)));
-      }
+    for (int e = 0; e < 4; ++e) {  // Vᵀ[d][row0], Vᵀ[d][row0 + 1] as one 32-bit store per plane
+      const int vo = (4 * ch + e) * VT3 + row0;
+      const unsigned sh = 16 * (e & 1);
+      *(unsigned*)&vp[slot][0][vo] = ((vh[0][e >> 1] >> sh) & 0xFFFFu) | ((vh[1][e >> 1] >> sh) << 16);
+      *(unsigned*)&vp[slot][1][vo] = ((vl[0][e >> 1] >> sh) & 0xFFFFu) | ((vl[1][e >> 1] >> sh) << 16);
     }
   };
 
@@ -282,13 +286,20 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
     for (int e = 0; e < 4; ++e) o[f][e] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
+  // K/V staging runs one tile ahead and beside the MFMAs: in iteration kt the registers loaded in
+  // iteration kt-1 (tile kt+1) are split into the other slot — whose last reader, tile kt-1, finished
+  // before the previous barrier — and the global loads of tile kt+2 are issued; one barrier per tile.
   const int nkt = (p.Sk + KT - 1) / KT;
   gload(0);
   lstore(0);
+  if (nkt > 1) gload(1);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int slot = kt & 1;
-    if (kt + 1 < nkt) gload(kt + 1);
+    if (kt + 1 < nkt) {
+      lstore(slot ^ 1);
+      if (kt + 2 < nkt) gload(kt + 2);
+    }
     const unsigned short* kh = kp[slot][0];
     const unsigned short* kl = kp[slot][1];
     const unsigned short* vh = vp[slot][0];
@@ -334,14 +345,14 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m[f], mx);
-      const float alpha = exp2f(m[f] - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m[f] - mn);
       m[f] = mn;
       float sum = 0.f;
 #pragma unroll
       for (int g = 0; g < KFR; ++g)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pv = exp2f(s[f][g][r] - mn);
+          const float pv = __builtin_amdgcn_exp2f(s[f][g][r] - mn);  // v_exp_f32 (no denormal fix-up)
           s[f][g][r] = pv;
           sum += pv;
         }
@@ -371,10 +382,6 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
       }
     }
     __syncthreads();
-    if (kt + 1 < nkt) {
-      lstore(slot ^ 1);
-      __syncthreads();
-    }
   }
 #pragma unroll
   for (int f = 0; f < QF; ++f) {
