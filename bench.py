@@ -342,7 +342,7 @@ def main():
                 roof["attention"] = {"kernel": an, "achieved": round(att, 1), "peak": apk, "unit": "TFLOP/s",
                                      "frac": round(att / apk, 4)}
     cpu = None
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:  # the CPU leg is an N = 1 figure
         cpu = _cpu_baseline(a.cpu_768_runs)
     if rank == 0:
         line = {
