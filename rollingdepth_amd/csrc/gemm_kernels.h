@@ -37,7 +37,18 @@ struct GemmP {
   const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
   int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
   int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
+  unsigned long long* stamps;  // STAMP builds only (tools/conv_stamp.hip): per-wave segment cycle sums
 };
+
+// In-kernel stamp (diagnostic builds, STAMP = 1; guide §7 'In-kernel stamps'): s_memtime with the
+// lgkmcnt(0) it needs in one statement, fenced from the scheduler on both sides.
+__device__ __forceinline__ unsigned long long gk_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
 
 // vmcnt(n) alone (gfx9 s_waitcnt encoding: vmcnt[3:0] | vmcnt[5:4]<<14, expcnt/lgkmcnt at max)
 template <int N>
@@ -1209,8 +1220,20 @@ __device__ __forceinline__ void occ2_sched(std::integer_sequence<int, S...>) {
 // fragment reads and 64 MFMAs.  At a channel block's first tap the halo is refilled in place:
 // barrier (all reads of the previous block's halo done), DMA, wait, [GroupNorm+SiLU of the own
 // pieces], barrier.
-template <int MODE, bool GN, bool PIPE>
+// STAMP = 1 (diagnostic build only, tools/conv_stamp.hip): per-wave cycle sums of the segments —
+// 0 prologue, 1 K-tile wait + barrier, 2 fragment reads + MFMA issue, 3 halo refill (barrier, DMA,
+// wait, GroupNorm transform, barrier), 4 epilogue, 5 total — written to p.stamps.
+template <int MODE, bool GN, bool PIPE, int STAMP = 0>
 __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
+  unsigned long long st_acc[6] = {}, st_prev = 0, st_start = 0;
+  auto seg = [&](int i) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const unsigned long long t = gk_stamp();
+      st_acc[i] += t - st_prev;
+      st_prev = t;
+    }
+  };
+  if constexpr (STAMP) st_start = st_prev = gk_stamp();
   constexpr int BN = 128, BKP = 64, RM = 8, RN = 4;
   constexpr int HWD = 18, HPIX = HWD * HWD;
   constexpr int HPC = 41;                  // pieces of 8 halo pixels (41·8 = 328 >= 324)
@@ -1343,10 +1366,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   asm volatile("" ::: "memory");
 
   const int wms = __builtin_amdgcn_readfirstlane(wm);
+  seg(0);
   for (int u = 0; u < nk; ++u) {
     const int cb = u / 9;
     const int tap = u - cb * 9;
     const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+    if (u > 0) seg(2);
     if (u > 0) {
       if (tap == 0) {  // refill the halo with channel block cb
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1362,6 +1387,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if (tap == 0) seg(3); else seg(1);
     }
     if (u + 1 < nk) issueB(u + 1);
     const f16* lb = lds + HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
@@ -1416,7 +1442,19 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
     }
   }
+  seg(2);
   store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+  if constexpr (STAMP) {
+    wait_vmcnt<0>();
+    seg(4);
+    st_acc[5] = st_prev - st_start;
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + (((long)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wid) * 8;
+      for (int i = 0; i < 6; ++i) o[i] = st_acc[i];
+      o[6] = st_start;
+      o[7] = st_prev;
+    }
+  }
 }
 
 // Halo conv with 32×32×16 MFMAs for 128-channel output tiles (the VAE's 768² / 384² convs with
