@@ -138,6 +138,11 @@ __device__ __forceinline__ void gn_xform_words(unsigned (&w)[NW], const float* s
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, unsigned voff, f16* l) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, 0, 0, 0);
 }
+// ... with a wave-uniform byte offset in the scalar soffset operand (a per-K-tile step that costs no
+// VALU); lanes whose voff is OOB stay out of range.
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff, f16* l) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, soff, 0, 0);
+}
 
 // Epilogue shared by both engines.  The MFMA ran as Dᵀ = W·Aᵀ, so a lane holds 4 CONSECUTIVE
 // output channels n = fq*4 + r of one row m = lane&15: bias / time-embedding / residual are read
@@ -1268,7 +1273,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   const int lrow = lane >> 3;
   const int chunk = (lane & 7) ^ lrow;
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
-  int hoff[HPW];  // piece t = wid + 4e: halo pixels 8t + lrow
+  unsigned hvo[HPW];  // piece t = wid + 4e: halo pixels 8t + lrow — byte offset at channel block 0, or OOB
 #pragma unroll
   for (int e = 0; e < HPW; ++e) {
     const int hp = (wid + 4 * e) * 8 + lrow;
@@ -1276,14 +1281,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
     const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
-    hoff[e] = ok ? ((b * p.IH + sy) * p.IW + sx) * p.Cin : -1;
+    hvo[e] = ok ? (unsigned)(((b * p.IH + sy) * p.IW + sx) * p.Cin + chunk * 8) * 2u : OOB;
   }
-  int brow[NB];
+  unsigned bvo[NB];  // weight DMA byte offsets of this lane's rows at K-tile 0 (the K step goes in soffset)
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
     const int rt = (wid + 4 * e) * 8 + lrow;  // LDS row of the tile
     const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
-    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+    bvo[e] = n < p.N ? (unsigned)(n * (int)p.ldw + chunk * 8) * 2u : OOB;
   }
   const int ncb = p.Cin >> 6;
   auto hv = [&](int e) { return wids + 4 * e < HPC; };
@@ -1292,18 +1297,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     for (int e = 0; e < HPW; ++e)
       if (hv(e)) {
         f16* lh = lds + (wid + 4 * e) * 8 * BKP;
-        dma16(ra_, hoff[e] >= 0 ? (unsigned)(hoff[e] + cb * 64 + chunk * 8) * 2u : OOB, lh);
+        dma16s(ra_, hvo[e], cb * 128, lh);
       }
   };
-  auto issueB = [&](int u) {
-    const int kk = u * BKP + chunk * 8;
-    const bool kok = kk < p.Kvalid;
+  auto issueB = [&](int u) {  // Kvalid % 64 == 0 (halo convs: 9 or 4 taps of Cin % 64 == 0)
     f16* lb = lds + HALO + (u & 1) * BSLOT;
 #pragma unroll
-    for (int e = 0; e < NB; ++e) {
-      const bool ok = brow[e] >= 0 && kok;
-      dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 4 * e) * 8 * BKP);
-    }
+    for (int e = 0; e < NB; ++e) dma16s(rw_, bvo[e], u * BKP * 2, lb + (wid + 4 * e) * 8 * BKP);
   };
   // in-place GroupNorm (+SiLU) of this wave's landed pieces of the halo of channel block cb
   auto xformHalo = [&](int cb) {
@@ -1318,7 +1318,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
         f16* lh = lds + (wid + 4 * e) * 8 * BKP + lane * 8;
         unsigned w[4];
         *(f16x8*)w = *(const f16x8*)lh;
-        const bool in = hoff[e] >= 0;
+        const bool in = hvo[e] != OOB;
         if (p.gsilu)  // the SiLU flag dispatched once per piece (see gn_elem)
           gn_xform_words<4, true>(w, sc, sh, in);
         else
@@ -1392,9 +1392,16 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     if (u + 1 < nk) issueB(u + 1);
     const f16* lb = lds + HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
     const int xb = fr + dx + 2 * dy;
+    // A fragment (kh, i): halo row wms·RM + i + dy, pixel dx + fr, 16-B chunk (kh·4 + fq) ^ ((xb + 2i) & 7).
+    // The swizzle has period 4 in i and kh = 1 flips chunk bit 2, so four lane byte offsets per K-tile
+    // serve all 16 reads: rows i and i + 4 differ by a DS immediate, kh = 1 is the offset ^ 64.
+    const unsigned abase = (unsigned)(((wms * RM + dy) * HWD + dx + fr) * BKP * 2);
+    unsigned aoff[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) aoff[r] = abase + (unsigned)((fq ^ ((xb + 2 * r) & 7)) << 4);
     auto readA = [&](int kh, int i) {
-      const f16* row = lds + ((wms * RM + i + dy) * HWD + dx) * BKP;
-      return *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
+      const unsigned a = kh ? (aoff[i & 3] ^ 64u) : aoff[i & 3];
+      return *(const f16x8*)((const char*)lds + a + i * HWD * BKP * 2);
     };
     if constexpr (PIPE) {
       // Software-pipelined fragment reads over the K-tile's 16 MFMA groups s = (kh, i): A(s+2) is

@@ -92,7 +92,11 @@ int main(int argc, char** argv) {
       best = std::min(best, ms);
     }
     CK(hipGetLastError());
-    printf("%s: %.3f ms  %.1f TF/s\n", variant ? "stamped" : "product", best, fl / best / 1e9);
+    std::vector<unsigned short> yh(M * Cout);
+    CK(hipMemcpy(yh.data(), y, M * Cout * 2, hipMemcpyDeviceToHost));
+    unsigned long long hsh = 1469598103934665603ull;  // FNV-1a of the output bits (A/B: bitwise equality)
+    for (unsigned short v : yh) hsh = (hsh ^ v) * 1099511628211ull;
+    printf("%s: %.3f ms  %.1f TF/s  output fnv %016llx\n", variant ? "stamped" : "product", best, fl / best / 1e9, hsh);
   }
   std::vector<unsigned long long> h(nw * 8);
   CK(hipMemcpy(h.data(), st, nw * 8 * 8, hipMemcpyDeviceToHost));
