@@ -963,7 +963,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   const int chunk = (lane & 7) ^ lrow;  // logical chunk fetched: piece pixels start at multiples of 8
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
   // halo pieces of this wave: t = wid + 8e → halo pixels hp = 8t + lrow (hp < 324 used)
-  int hoff[HPW];
+  unsigned hvo[HPW];  // byte offsets at channel block 0 (the block step goes in soffset), or OOB
 #pragma unroll
   for (int e = 0; e < HPW; ++e) {
     const int hp = (wid + 8 * e) * 8 + lrow;
@@ -971,32 +971,28 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     const int yy = y0 - 1 + pa + hr, xx = x0 - 1 + pc + hc;
     const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
-    hoff[e] = ok ? ((b * p.IH + sy) * p.IW + sx) * p.Cin : -1;
+    hvo[e] = ok ? (unsigned)(((b * p.IH + sy) * p.IW + sx) * p.Cin + chunk * 8) * 2u : OOB;
   }
-  int brow[NB];
+  unsigned bvo[NB];  // weight byte offsets at K-tile 0 (the K step goes in soffset), or OOB
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
     const int rt = (wid + 8 * e) * 8 + lrow;  // LDS row of the tile
     const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
-    brow[e] = n < p.N ? (phs * p.N + n) * (int)p.ldw : -1;
+    bvo[e] = n < p.N ? (unsigned)((phs * p.N + n) * (int)p.ldw + chunk * 8) * 2u : OOB;
   }
   const int ncb = p.Cin >> 6;
   const int wids = __builtin_amdgcn_readfirstlane(wid);
   auto hv = [&](int e) { return wids + 8 * e < HPC; };  // piece slot e of this wave holds halo pixels
-  auto issueHalo = [&](int cb, int e) {
+  auto issueHalo = [&](int cb, int e) {  // past the last block: zero-fill DMAs (the wait counts stay fixed)
     f16* lh = lds + (cb & 1) * HALO + (wid + 8 * e) * 8 * BKP;
-    const bool ok = hoff[e] >= 0 && cb < ncb;
-    dma16(ra_, ok ? (unsigned)(hoff[e] + cb * 64 + chunk * 8) * 2u : OOB, lh);
+    const bool ok = cb < ncb;  // wave-uniform
+    dma16s(ra_, ok ? hvo[e] : OOB, ok ? cb * 128 : 0, lh);
   };
-  auto issueB = [&](int u, int e0, int e1) {
-    const int kk = u * BKP + chunk * 8;
-    const bool kok = kk < p.Kvalid;
+  auto issueB = [&](int u, int e0, int e1) {  // Kvalid % 64 == 0 (9 or 4 taps of Cin % 64 == 0)
     f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT;
+    const bool kok = u * BKP < p.Kvalid;  // wave-uniform
 #pragma unroll
-    for (int e = e0; e < e1; ++e) {
-      const bool ok = brow[e] >= 0 && kok;
-      dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 8 * e) * 8 * BKP);
-    }
+    for (int e = e0; e < e1; ++e) dma16s(rw_, kok ? bvo[e] : OOB, kok ? u * BKP * 2 : 0, lb + (wid + 8 * e) * 8 * BKP);
   };
 
   f32x4 acc[RM][RN];
@@ -1019,7 +1015,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     const f32x4 sc = *(const f32x4*)ts, sh = *(const f32x4*)(ts + GNT);
     unsigned w[2];
     *(f16x4*)w = *(const f16x4*)lh;
-    const bool in = hoff[e] >= 0;
+    const bool in = hvo[e] != OOB;
     const float scv[4] = {sc[0], sc[1], sc[2], sc[3]}, shv[4] = {sh[0], sh[1], sh[2], sh[3]};
     if (p.gsilu)  // the SiLU flag dispatched once per piece, not tested per element
       gn_xform_words<2, true>(w, scv, shv, in);
@@ -1079,12 +1075,17 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     const int cb = u / NT;  // wave-uniform
     const int tap = u - cb * NT;
     const int dy = MODE == 3 ? tap >> 1 : (tap * 11) >> 5, dx = MODE == 3 ? tap & 1 : tap - 3 * dy;
-    const f16* lh = lds + (cb & 1) * HALO;
     const f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT + (wn * 64) * BKP;
     const bool halo_now = MODE != 3 && tap >= 1 && tap <= HPW && hv(tap - 1);
     // halo pixel of fragment row r = RM·wm + 4·rg + i, lane fr: hp = (r + dy)·18 + dx + fr, whose
     // swizzle term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or rg (RM·18, 72 ≡ 0 mod 8)
     const int xb = fr + dx + 2 * dy;
+    // A fragment (kh, rg, i): halo row wms·RM + 4·rg + i + dy, pixel dx + fr, chunk (kh·4 + fq) ^ ((xb + 2i) & 7):
+    // four lane byte offsets per K-tile; row group rg by DS immediate, kh = 1 as the offset ^ 64
+    const unsigned abase = (unsigned)((cb & 1) * HALO * 2 + ((wms * RM + dy) * HWD + dx + fr) * BKP * 2);
+    unsigned aoff[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) aoff[r] = abase + (unsigned)((fq ^ ((xb + 2 * r) & 7)) << 4);
 #pragma unroll
     for (int ph = 0; ph < NPH; ++ph) {
       const int rg = NPH == 4 ? ph >> 1 : ph;
@@ -1102,10 +1103,8 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
           for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f16* row = lh + ((wms * RM + rg * 4 + i + dy) * HWD + dx) * BKP;
-          af[q][i] = *(const f16x8*)(row + fr * BKP + (((kh * 4 + fq) ^ ((xb + 2 * i) & 7)) << 3));
-        }
+        for (int i = 0; i < 4; ++i)
+          af[q][i] = *(const f16x8*)((const char*)lds + (kh ? aoff[i] ^ 64u : aoff[i]) + (rg * 4 + i) * HWD * BKP * 2);
       }
       if (NPH == 4) {
         if (ph == 0) {

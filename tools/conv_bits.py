@@ -1,0 +1,50 @@
+"""Bit fingerprints of the implicit-GEMM engines' outputs at the pipeline's shapes, for A/B builds that
+must be bitwise equal (addressing-only changes): run once per library (RDMI_LIB=...) and diff.
+
+    python tools/conv_bits.py > a.txt; RDMI_LIB=old.so python tools/conv_bits.py > b.txt; diff a.txt b.txt
+"""
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from rollingdepth_amd import kernels as K  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kbench import conv_cases  # noqa: E402
+
+
+def fp(t: torch.Tensor) -> str:
+    v = t.contiguous().view(torch.int16).flatten().to(torch.int64)
+    w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 65521 + 1
+    return f"{int(v.sum())} {int((v * w).sum() % (1 << 61))}"
+
+
+def main():
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for lab, B, H, W, ci, co, up in conv_cases():
+        B = min(B, 4)
+        x = torch.randn(B, H, W, ci, device="cuda", generator=g).half()
+        w = K.pack_conv(torch.randn(co, ci, 3, 3, generator=torch.Generator().manual_seed(1)) / math.sqrt(ci * 9),
+                        "cuda", ci)
+        Ho, Wo = (2 * H, 2 * W) if up else (H, W)
+        out = K.conv2d(x, w, co, 3, upsample=up)
+        print(f"conv   {lab:32s} {fp(out)}")
+        gm, bt = torch.rand(ci, device="cuda", generator=g) + 0.5, torch.randn(ci, device="cuda", generator=g) * 0.1
+        if K.conv2d_in_gn_supported(x, w, co, 3, 32, upsample=up):
+            mr = K.groupnorm_stats(x, 32, 1e-6)
+            res = torch.randn(B, Ho, Wo, co, device="cuda", generator=g).half()
+            o2 = K.conv2d(x, w, co, 3, upsample=up, in_gn=(mr, gm, bt, 32, True), residual=res, gn=True)
+            o2 = o2[0] if isinstance(o2, tuple) else o2
+            print(f"gnconv {lab:32s} {fp(o2)}")
+    for M, N, Kd in [(4096, 320, 320), (4096, 2560, 320), (2048, 1280, 1280), (4096, 960, 320), (1024, 10240, 1280)]:
+        a = torch.randn(M, Kd, device="cuda", generator=g).half()
+        wl = (torch.randn(N, Kd, device="cuda", generator=g) / math.sqrt(Kd)).half()
+        print(f"gemm   M={M} N={N} K={Kd}{'':12s} {fp(K.gemm(a, wl, Kd))}")
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,11 @@
+# 256-wide halo conv K-loop addressing: output bits vs the previous library (tools/librdmi_ab_old.so),
+# kbench conv / gnconv A/B, conv parity tests, fast-preset bench.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 200 python -u tools/conv_bits.py > gpurun_out/r03p_bits_new.txt 2>&1 || exit $?
+RDMI_LIB=tools/librdmi_ab_old.so timeout -k 10 200 python -u tools/conv_bits.py > gpurun_out/r03p_bits_old.txt 2>&1 || exit $?
+( diff gpurun_out/r03p_bits_old.txt gpurun_out/r03p_bits_new.txt && echo "BITWISE EQUAL" ) > gpurun_out/r03p_bits_diff.txt 2>&1 || true
+( RDMI_LIB=tools/librdmi_ab_old.so timeout -k 10 200 python -u tools/kbench.py --only conv,gnconv --iters 20 | sed 's/^/old /' && timeout -k 10 200 python -u tools/kbench.py --only conv,gnconv --iters 20 | sed 's/^/new /' ) > gpurun_out/r03p_kbench_ab.log 2>&1 || exit $?
+bash tools/hb.sh timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "conv or halo or up2" > gpurun_out/r03p_conv_tests.log 2>&1 || exit $?
+bash tools/hb.sh timeout -k 10 400 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/r03p_bench.log 2>&1 || exit $?
