@@ -670,6 +670,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  const int wids = __builtin_amdgcn_readfirstlane(wid);  // DMA LDS destinations in SGPRs (M0)
   const int grp = wid >> 2;
   const int wm = wid / WN, wn = wid % WN;
   const int nbx = gridDim.x;
@@ -713,27 +714,29 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
         arow[h][e] = mm * (int)p.lda;
       }
     }
-  int brow[NB];
+  unsigned bvo[NB];  // weight byte offsets of this lane's rows at K-tile 0 (the K step goes in soffset), or OOB
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
     const int n = n0 + (wid + 8 * e) * 8 + lrow;
-    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+    bvo[e] = n < p.N ? (unsigned)(n * (int)p.ldw + chunk * 8) * 2u : OOB;
   }
+  unsigned avo[2][NA];  // MODE 0: the same for the A rows
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < NA; ++e) avo[h][e] = ahb[h][e] == 0 ? (unsigned)(arow[h][e] + chunk * 8) * 2u : OOB;
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
 
   // A pieces e in [e0, e1) of half h, K-tile u
   auto issueA = [&](int h, int u, int e0, int e1) {
     f16* la = lds + (u & 1) * SLOT;
     if (MODE == 0) {
-      const int kk = u * BKP + chunk * 8;
-      const bool kok = kk < p.Kvalid;
+      const bool kok = u * BKP + chunk * 8 < p.Kvalid;  // lane-dependent only in a ragged last K-tile
 #pragma unroll
       for (int e = 0; e < NA; ++e) {
         if (e < e0 || e >= e1) continue;
-        const int t = wid + 8 * e;
-        const bool ok = ahb[h][e] == 0 && kok;
-        dma16(ra_, ok ? (unsigned)(arow[h][e] + kk) * 2u : OOB,
-              la + ((t >> 3) * 128 + h * 64 + (t & 7) * 8) * BKP);
+        const int t = wids + 8 * e;
+        dma16s(ra_, kok ? avo[h][e] : OOB, u * BKP * 2, la + ((t >> 3) * 128 + h * 64 + (t & 7) * 8) * BKP);
       }
     } else {
       const int cb = u / 9;  // wave-uniform
@@ -745,7 +748,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 #pragma unroll
       for (int e = 0; e < NA; ++e) {
         if (e < e0 || e >= e1) continue;
-        const int t = wid + 8 * e;
+        const int t = wids + 8 * e;
         const int hi = ahb[h][e] + dy, wi = awb[h][e] + dx;
         const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
         int off;
@@ -759,14 +762,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
   };
   // B pieces e in [e0, e1) of K-tile u
   auto issueB = [&](int u, int e0, int e1) {
-    const int kk = u * BKP + chunk * 8;
-    const bool kok = kk < p.Kvalid;
+    const bool kok = u * BKP + chunk * 8 < p.Kvalid;
     f16* lb = lds + (u & 1) * SLOT + BM * BKP;
 #pragma unroll
     for (int e = 0; e < NB; ++e) {
       if (e < e0 || e >= e1) continue;
-      const bool ok = brow[e] >= 0 && kok;
-      dma16(rw_, ok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 8 * e) * 8 * BKP);
+      dma16s(rw_, kok ? bvo[e] : OOB, u * BKP * 2, lb + (wids + 8 * e) * 8 * BKP);
     }
   };
 
@@ -984,7 +985,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   const int wids = __builtin_amdgcn_readfirstlane(wid);
   auto hv = [&](int e) { return wids + 8 * e < HPC; };  // piece slot e of this wave holds halo pixels
   auto issueHalo = [&](int cb, int e) {  // past the last block: zero-fill DMAs (the wait counts stay fixed)
-    f16* lh = lds + (cb & 1) * HALO + (wid + 8 * e) * 8 * BKP;
+    f16* lh = lds + (cb & 1) * HALO + (wids + 8 * e) * 8 * BKP;
     const bool ok = cb < ncb;  // wave-uniform
     dma16s(ra_, ok ? hvo[e] : OOB, ok ? cb * 128 : 0, lh);
   };
@@ -992,7 +993,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT;
     const bool kok = u * BKP < p.Kvalid;  // wave-uniform
 #pragma unroll
-    for (int e = e0; e < e1; ++e) dma16s(rw_, kok ? bvo[e] : OOB, kok ? u * BKP * 2 : 0, lb + (wid + 8 * e) * 8 * BKP);
+    for (int e = e0; e < e1; ++e) dma16s(rw_, kok ? bvo[e] : OOB, kok ? u * BKP * 2 : 0, lb + (wids + 8 * e) * 8 * BKP);
   };
 
   f32x4 acc[RM][RN];
@@ -1295,14 +1296,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
 #pragma unroll
     for (int e = 0; e < HPW; ++e)
       if (hv(e)) {
-        f16* lh = lds + (wid + 4 * e) * 8 * BKP;
+        f16* lh = lds + (wids + 4 * e) * 8 * BKP;
         dma16s(ra_, hvo[e], cb * 128, lh);
       }
   };
   auto issueB = [&](int u) {  // Kvalid % 64 == 0 (halo convs: 9 or 4 taps of Cin % 64 == 0)
     f16* lb = lds + HALO + (u & 1) * BSLOT;
 #pragma unroll
-    for (int e = 0; e < NB; ++e) dma16s(rw_, bvo[e], u * BKP * 2, lb + (wid + 4 * e) * 8 * BKP);
+    for (int e = 0; e < NB; ++e) dma16s(rw_, bvo[e], u * BKP * 2, lb + (wids + 4 * e) * 8 * BKP);
   };
   // in-place GroupNorm (+SiLU) of this wave's landed pieces of the halo of channel block cb
   auto xformHalo = [&](int cb) {
@@ -1805,6 +1806,7 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  const int wids = __builtin_amdgcn_readfirstlane(wid);  // DMA LDS destinations in SGPRs (M0)
   const int wm = wid >> 1, wn = wid & 1;
   const int nbx = gridDim.x;
   const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
@@ -1819,28 +1821,25 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
 
   const int lrow = lane >> 3;
   const int chunk = (lane & 7) ^ lrow;
-  int arow[NA], brow[NB];
+  unsigned avo[NA], bvo[NB];  // byte offsets of this lane's rows at K-tile 0 (the K step goes in soffset), or OOB
 #pragma unroll
   for (int e = 0; e < NA; ++e) {
     const int m = m0 + (wid + 4 * e) * 8 + lrow;
-    arow[e] = m < p.M ? m * (int)p.lda : -1;
+    avo[e] = m < p.M ? (unsigned)(m * (int)p.lda + chunk * 8) * 2u : OOB;
   }
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
     const int n = n0 + (wid + 4 * e) * 8 + lrow;
-    brow[e] = n < p.N ? n * (int)p.ldw : -1;
+    bvo[e] = n < p.N ? (unsigned)(n * (int)p.ldw + chunk * 8) * 2u : OOB;
   }
   auto issue = [&](int u) {
-    const int kk = u * BKP + chunk * 8;
-    const bool kok = kk < p.Kvalid;
+    const bool kok = u * BKP + chunk * 8 < p.Kvalid;  // lane-dependent only in a ragged last K-tile
     f16* la = lds + (u & 1) * SLOT;
     f16* lb = la + BM * BKP;
 #pragma unroll
-    for (int e = 0; e < NA; ++e)
-      dma16(ra_, arow[e] >= 0 && kok ? (unsigned)(arow[e] + kk) * 2u : OOB, la + (wid + 4 * e) * 8 * BKP);
+    for (int e = 0; e < NA; ++e) dma16s(ra_, kok ? avo[e] : OOB, u * BKP * 2, la + (wids + 4 * e) * 8 * BKP);
 #pragma unroll
-    for (int e = 0; e < NB; ++e)
-      dma16(rw_, brow[e] >= 0 && kok ? (unsigned)(brow[e] + kk) * 2u : OOB, lb + (wid + 4 * e) * 8 * BKP);
+    for (int e = 0; e < NB; ++e) dma16s(rw_, kok ? bvo[e] : OOB, u * BKP * 2, lb + (wids + 4 * e) * 8 * BKP);
   };
 
   f32x4 acc[RM][RN];

@@ -39,6 +39,14 @@ def main():
             o2 = K.conv2d(x, w, co, 3, upsample=up, in_gn=(mr, gm, bt, 32, True), residual=res, gn=True)
             o2 = o2[0] if isinstance(o2, tuple) else o2
             print(f"gnconv {lab:32s} {fp(o2)}")
+    # implicit-GEMM (non-halo) conv modes: nearest-x2 upsample at 12 -> 24 (Ho % 16 != 0), stride 2
+    for lab, B, H, ci, co, kw in [("up 1280 12->24", 4, 12, 1280, 1280, dict(upsample=True)),
+                                  ("s2 320 96->48", 4, 96, 320, 320, dict(stride=2)),
+                                  ("s2 128 768->384", 1, 768, 128, 128, dict(stride=2))]:
+        x = torch.randn(B, H, H, ci, device="cuda", generator=g).half()
+        w = K.pack_conv(torch.randn(co, ci, 3, 3, generator=torch.Generator().manual_seed(2)) / math.sqrt(ci * 9),
+                        "cuda", ci)
+        print(f"conv   {lab:32s} {fp(K.conv2d(x, w, co, 3, **kw))}")
     for M, N, Kd in [(4096, 320, 320), (4096, 2560, 320), (2048, 1280, 1280), (4096, 960, 320), (1024, 10240, 1280)]:
         a = torch.randn(M, Kd, device="cuda", generator=g).half()
         wl = (torch.randn(N, Kd, device="cuda", generator=g) / math.sqrt(Kd)).half()
