@@ -915,8 +915,20 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 // halo (origin (y0 − 1 + a, x0 − 1 + c)) sits in the 18×18 halo buffer; weights p.Wt + phase·N·ldw
 // in the cmaj order with 4 taps (dy, dx) ∈ {0, 1}²; halo(cb+1) pieces 0-2 issued in tap 1, 3-5 in
 // tap 2, all landed by tap 3's wait.
-template <int MODE, int NPH, int WN, bool GN>
+// STAMP = 1 (diagnostic build only, tools/conv_stamp.hip): per-wave cycle sums — 0 prologue, 1 load
+// sections (fragment reads, DMA issue, waits), 2 barrier before the MFMAs, 3 MFMA issue, 4 GroupNorm
+// transform, 5 barrier after, 6 epilogue, 7 total — written to p.stamps.
+template <int MODE, int NPH, int WN, bool GN, int STAMP = 0>
 __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
+  unsigned long long st_acc[8] = {}, st_prev = 0, st_start = 0;
+  auto seg = [&](int i) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const unsigned long long t = gk_stamp();
+      st_acc[i] += t - st_prev;
+      st_prev = t;
+    }
+  };
+  if constexpr (STAMP) st_start = st_prev = gk_stamp();
   constexpr int NT = MODE == 3 ? 4 : 9;    // taps per channel block
   constexpr int WM = 8 / WN;
   constexpr int BN = WN * 64, BKP = 64, RM = 16 / WM, RN = 4;
@@ -1072,6 +1084,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
 
   const int wms = __builtin_amdgcn_readfirstlane(wm);
   f16x8 af[NKH][4] = {}, bf[2][RN] = {};
+  seg(0);
   for (int u = 0; u < nk; ++u) {
     const int cb = u / NT;  // wave-uniform
     const int tap = u - cb * NT;
@@ -1160,9 +1173,11 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
           wait_vmcnt<NB>();  // B(u+1) (and on tap 7 all of halo(cb+1)) landed (B(u+2) in flight)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
+      seg(1);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      seg(2);
       // ---- MFMA(NPH·u + ph)
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1175,6 +1190,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
             acc[rg * 4 + i][j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[q][i], acc[rg * 4 + i][j], 0, 0, 0);
       }
+      seg(3);
       if (xf) {  // after this wave's MFMAs (interleaved between them, or with its operands read
                  // in the load segment, it measured slower: tools/kbench.py gnconv)
         if (NPH == 1 || ph == 1) xform(cb + 1, xe, 0);
@@ -1182,19 +1198,31 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
       }
       __builtin_amdgcn_s_setprio(0);
       if (xf) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // normalised values written
+      seg(4);
       asm volatile("" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      seg(5);
     }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();  // match group 1's extra barrier
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
+  seg(5);
 
   if constexpr (MODE == 3)
     store_tile<RM, RN, 64>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr, fq,
                            p.cperm);
   else
     store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+  if constexpr (STAMP) {
+    wait_vmcnt<0>();
+    seg(6);
+    st_acc[7] = st_prev - st_start;
+    if (lane == 0) {
+      unsigned long long* o = p.stamps + (((long)blockIdx.y * gridDim.x + blockIdx.x) * 8 + wid) * 8;
+      for (int i = 0; i < 8; ++i) o[i] = st_acc[i];
+    }
+  }
 }
 
 // Issue-order pins for conv_halo_occ2_kernel's pipelined K-tile (sched_group_barrier needs

@@ -4,7 +4,8 @@
 // 128-channel shape: 768² 128 → 128, B images, GroupNorm+SiLU input, residual and GroupNorm moments
 // out (the VAE ResnetBlock2D conv2).  Read the SHARES, not the stamped build's run time.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/conv_stamp.hip -o tools/conv_stamp
-//   ./tools/conv_stamp [B] [HW] [gn res moments: 0/1 each]
+//   ./tools/conv_stamp [B] [HW] [gn res moments: 0/1 each] [Cin] [Cout]
+// Cout = 128: conv_halo_occ2_kernel; Cout % 256 == 0: conv_halo_kernel<1, 2, 4, GN> (8 waves, ping-pong).
 #include "../rollingdepth_amd/csrc/gemm_kernels.h"
 
 #include <algorithm>
@@ -35,17 +36,25 @@ __global__ void fill_f(float* x, long n, float a, float b) {
 }
 
 template <int ST>
-void launch(dim3 g, const GemmP& p) {
-  if (p.gmr)
+void launch(dim3 g, const GemmP& p, bool wide) {
+  if (wide) {
+    if (p.gmr)
+      hipLaunchKernelGGL((conv_halo_kernel<1, 2, 4, true, ST>), g, dim3(512), 0, 0, p);
+    else
+      hipLaunchKernelGGL((conv_halo_kernel<1, 2, 4, false, ST>), g, dim3(512), 0, 0, p);
+  } else if (p.gmr) {
     hipLaunchKernelGGL((conv_halo_occ2_kernel<1, true, true, ST>), g, dim3(256), 0, 0, p);
-  else
+  } else {
     hipLaunchKernelGGL((conv_halo_occ2_kernel<1, false, true, ST>), g, dim3(256), 0, 0, p);
+  }
 }
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 8, HW = argc > 2 ? atoi(argv[2]) : 768;
   const bool gn = argc > 3 ? atoi(argv[3]) : 1, res = argc > 4 ? atoi(argv[4]) : 1, mom = argc > 5 ? atoi(argv[5]) : 1;
-  const int Cin = 128, Cout = 128, Kp = 9 * Cin, G = 32;
+  const int Cin = argc > 6 ? atoi(argv[6]) : 128, Cout = argc > 7 ? atoi(argv[7]) : 128, Kp = 9 * Cin, G = 32;
+  const bool wide = Cout % 256 == 0;
+  const int WPG = wide ? 8 : 4;  // waves per workgroup
   const long M = (long)B * HW * HW;
   f16 *x, *w, *y, *r;
   float *gmr, *gam, *bet, *gnp;
@@ -70,8 +79,8 @@ int main(int argc, char** argv) {
   p.a_bytes = (unsigned)(M * Cin * 2); p.w_bytes = (unsigned)((long)Cout * Kp * 2);
   p.group_m = 8; p.cperm = 1; p.conv_pipe = 1;
   if (gn) { p.gmr = gmr; p.ggam = gam; p.gbet = bet; p.gG = G; p.gsilu = 1; }
-  const dim3 g(1, (unsigned)((HW / 16) * (HW / 16) * B), 1);
-  const long nw = (long)g.y * 4;
+  const dim3 g(wide ? Cout / 256 : 1, (unsigned)((HW / 16) * (HW / 16) * B), 1);
+  const long nw = (long)g.x * g.y * WPG;
   unsigned long long* st;
   CK(hipMalloc(&st, nw * 8 * 8));
   p.stamps = st;
@@ -84,7 +93,7 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int rep = 0; rep < 8; ++rep) {
       CK(hipEventRecord(e0, 0));
-      if (variant == 0) launch<0>(g, p); else launch<1>(g, p);
+      if (variant == 0) launch<0>(g, p, wide); else launch<1>(g, p, wide);
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -100,18 +109,16 @@ int main(int argc, char** argv) {
   }
   std::vector<unsigned long long> h(nw * 8);
   CK(hipMemcpy(h.data(), st, nw * 8 * 8, hipMemcpyDeviceToHost));
-  const char* names[6] = {"prologue", "K-tile wait+barrier", "reads+MFMA issue", "halo refill", "epilogue", "total"};
-  double sum[6] = {};
-  unsigned long long t0 = ~0ull, t1 = 0;
-  for (long i = 0; i < nw; ++i) {
-    for (int s = 0; s < 6; ++s) sum[s] += (double)h[i * 8 + s];
-    t0 = std::min(t0, h[i * 8 + 6]);
-    t1 = std::max(t1, h[i * 8 + 7]);
-  }
+  const char* occ2_names[6] = {"prologue", "K-tile wait+barrier", "reads+MFMA issue", "halo refill", "epilogue", "total"};
+  const char* wide_names[8] = {"prologue", "load sections", "barrier before MFMA", "MFMA issue", "GroupNorm transform",
+                               "barrier after", "epilogue", "total"};
+  const int ns = wide ? 8 : 6, tot = ns - 1;
+  double sum[8] = {};
+  for (long i = 0; i < nw; ++i)
+    for (int s = 0; s < ns; ++s) sum[s] += (double)h[i * 8 + s];
   printf("per wave (mean s_memtime ticks, %ld waves):\n", nw);
-  for (int s = 0; s < 6; ++s) printf("  %-22s %10.0f  %5.1f %%\n", names[s], sum[s] / nw, 100.0 * sum[s] / sum[5]);
-  // the MFMA work of one wave: 18 K-tiles x 64 MFMA (16x16x32 f16, 8 passes = 16 cycles at the shader clock)
-  printf("  (one wave's MFMA work: 18 K-tiles x 64 16x16x32 MFMAs x 16 cycles = 18432 cycles)\n");
-  printf("stamped kernel span: %.0f s_memtime ticks (shader-clock cycles)\n", (double)(t1 - t0));
+  for (int s = 0; s < ns; ++s)
+    printf("  %-22s %10.0f  %5.1f %%\n", wide ? wide_names[s] : occ2_names[s], sum[s] / nw, 100.0 * sum[s] / sum[tot]);
+  printf("  (one wave's MFMA work: %d K-tiles x 64 16x16x32 MFMAs x 16 cycles = %d cycles)\n", Kp / 64, Kp / 64 * 1024);
   return 0;
 }
