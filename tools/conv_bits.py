@@ -51,6 +51,11 @@ def main():
         a = torch.randn(M, Kd, device="cuda", generator=g).half()
         wl = (torch.randn(N, Kd, device="cuda", generator=g) / math.sqrt(Kd)).half()
         print(f"gemm   M={M} N={N} K={Kd}{'':12s} {fp(K.gemm(a, wl, Kd))}")
+    # flash attention (attn_fwd_d64): a fused-QKV layout at the L0 / L1 shapes and ragged key counts
+    for B, S, H in [(2, 27648, 5), (2, 6912, 10), (1, 1000, 5), (1, 31, 2)]:
+        qkv = torch.randn(B, S, 3 * H * 64, device="cuda", generator=g).half()
+        q, k, v = qkv[..., :H * 64], qkv[..., H * 64:2 * H * 64], qkv[..., 2 * H * 64:]
+        print(f"attn   B={B} S={S} H={H}{'':18s} {fp(K.attention(q, k, v, H))}")
     torch.cuda.synchronize()
 
 
