@@ -128,12 +128,16 @@ bool vec_ok(const GemmP& p) {
 }
 
 // Halo engine (RDMI_CONV_HALO, read per launch for A/B measurements: 0 disables it, 1 = the
-// 4-phase variant where one exists, 3 = the two-workgroups-per-CU variant for every Cout % 128 ==
-// 0, 4 = the 8-wave variant for 128 output channels instead of the two-workgroups-per-CU one,
-// unset/2 = default).
+// 4-phase 256-wide variant where one exists, 2 = the 256-wide 8-wave ping-pong for Cout % 256 == 0,
+// 4 = the 8-wave variant for 128 output channels instead of the two-workgroups-per-CU one,
+// unset/3 = default: the two-workgroups-per-CU variant for every Cout % 128 == 0 conv except a
+// GroupNorm input wider than its 256-channel table.  Measured after the round-3 K-loop VALU cuts
+// (tools/kbench.py conv, profiles/r03x_kbench.log): +4–9 % on the VAE 512-channel 96² and upsample
+// convs, +6 % on the 384² GroupNorm conv, +1 % on the bench (r03x_halo_ab.log); bitwise the same
+// results as the 256-wide form (same K-tile order and MFMA operands per output, r03y_bits_diff.txt).
 int halo_mode() {
   const char* he = getenv("RDMI_CONV_HALO");
-  return he ? atoi(he) : 2;
+  return he ? atoi(he) : 3;
 }
 
 // 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 output patches,
@@ -257,7 +261,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
     const bool gn = p.gmr != nullptr;
-    if (a->upsample && a->w_up2 && !gn && a->Cout % 256 == 0 && a->Ho % 32 == 0 && a->Wo % 32 == 0 && hmode != 3 &&
+    if (a->upsample && a->w_up2 && !gn && a->Cout % 256 == 0 && a->Ho % 32 == 0 && a->Wo % 32 == 0 &&
         al16(a->w_up2)) {  // phase-decomposed ×2 upsample conv (4 taps per phase)
       p.Wt = (const f16*)a->w_up2; p.ldw = 4L * a->Cin; p.K = p.Kvalid = 4 * a->Cin;
       p.w_bytes = (unsigned)(4L * a->Cout * p.ldw * 2);

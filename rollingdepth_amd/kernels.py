@@ -397,9 +397,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
 
 def _up2_runs(a) -> bool:
     """Mirror of rdmi_conv2d's choice of the phase-decomposed upsample form (gemm.hip)."""
-    hm = int(os.environ.get("RDMI_CONV_HALO", "2"))
+    hm = int(os.environ.get("RDMI_CONV_HALO", "3"))
     return (a.upsample == 1 and bool(a.w_up2) and not a.in_mean_rstd and a.Cout % 256 == 0 and a.Ho % 32 == 0 and
-            a.Wo % 32 == 0 and hm not in (0, 3) and a.kh == 3 and a.kw == 3 and a.Cin % 64 == 0 and a.stride == 1 and
+            a.Wo % 32 == 0 and hm != 0 and a.kh == 3 and a.kw == 3 and a.Cin % 64 == 0 and a.stride == 1 and
             a.pad_top == 1 and a.pad_left == 1 and a.Ho == 2 * a.H and a.Wo == 2 * a.W)
 
 

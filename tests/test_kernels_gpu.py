@@ -18,17 +18,18 @@ def _k():
     return K
 
 
-@pytest.fixture(params=["auto", "classic", "pingpong", "halo4", "halo128w8"])
+@pytest.fixture(params=["auto", "classic", "pingpong", "halo4", "halo128w8", "halo256"])
 def engine(request, monkeypatch):
-    """GEMM/conv engine: by size (auto: halo conv with 2 phases per K-tile where it applies, the
-    two-workgroups-per-CU halo conv for 128 output channels, the two-workgroups-per-CU GEMM for
-    K ≤ 640), the 3-slot classic engine only, the ping-pong engine forced for every launch it
-    supports (N % 256 == 0), the 4-phase halo conv with the two-workgroups-per-CU GEMM for every
-    dense GEMM, or the 8-wave 128-channel halo conv (RDMI_GEMM_PP / RDMI_CONV_HALO /
-    RDMI_GEMM_OCC2, gemm.hip)."""
-    pp = {"auto": "1", "classic": "0", "pingpong": "2", "halo4": "1", "halo128w8": "1"}
-    halo = {"auto": "2", "classic": "0", "pingpong": "0", "halo4": "1", "halo128w8": "4"}
-    occ2 = {"auto": "1", "classic": "0", "pingpong": "0", "halo4": "2", "halo128w8": "0"}  # halo4: every dense GEMM
+    """GEMM/conv engine: by size (auto: the two-workgroups-per-CU halo conv for Cout % 128 == 0, the
+    two-workgroups-per-CU GEMM for K ≤ 640), the 3-slot classic engine only, the ping-pong engine
+    forced for every launch it supports (N % 256 == 0), the 4-phase halo conv with the
+    two-workgroups-per-CU GEMM for every dense GEMM, the 8-wave 128-channel halo conv, or the 256-wide
+    8-wave ping-pong halo conv for Cout % 256 == 0 (RDMI_GEMM_PP / RDMI_CONV_HALO / RDMI_GEMM_OCC2,
+    gemm.hip)."""
+    pp = {"auto": "1", "classic": "0", "pingpong": "2", "halo4": "1", "halo128w8": "1", "halo256": "1"}
+    halo = {"auto": "3", "classic": "0", "pingpong": "0", "halo4": "1", "halo128w8": "4", "halo256": "2"}
+    occ2 = {"auto": "1", "classic": "0", "pingpong": "0", "halo4": "2", "halo128w8": "0",
+            "halo256": "1"}  # halo4: every dense GEMM
     monkeypatch.setenv("RDMI_GEMM_PP", pp[request.param])
     monkeypatch.setenv("RDMI_CONV_HALO", halo[request.param])
     monkeypatch.setenv("RDMI_GEMM_OCC2", occ2[request.param])
