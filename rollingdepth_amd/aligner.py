@@ -14,14 +14,26 @@ import torch
 from . import kernels as K
 
 
+MAX_DILATIONS = 8   # aligner.hip MAXD
+MAX_ROWS = 64       # aligner.hip MAXR: Σ snippet lengths (rows of the reference's M / M_depth / B tensors)
+
+
 def check_row_layout(lengths: List[int], num_iterations: int) -> None:
     """The reference scatters dilation i's slots into rows i·w_i .. i·w_i + w_i − 1 of [Σw, N, P]
-    tensors (depth_aligner.py:169-188); rows past Σw raise its IndexError (first closure call)."""
+    tensors (depth_aligner.py:169-188); rows past Σw raise its IndexError (first closure call).
+    Also the limits of the aligner kernels (at most 8 dilations, at most 64 rows), checked here so
+    that forward() / sharded_forward() reject such a job before any inference runs rather than at
+    the aligner call after it."""
     rows = sum(lengths)
+    if len(lengths) > MAX_DILATIONS:
+        raise NotImplementedError(f"{len(lengths)} dilations: the aligner kernels take at most {MAX_DILATIONS}")
     if num_iterations > 0:
         for i, w in enumerate(lengths):
             if (i + 1) * w > rows:
                 raise IndexError(f"index {(i + 1) * w - 1} is out of bounds for dimension 0 with size {rows}")
+        if rows > MAX_ROWS:
+            raise NotImplementedError(f"snippet lengths {list(lengths)} sum to {rows} aligner rows: the aligner "
+                                      f"kernel takes at most {MAX_ROWS}")
 
 
 class DepthAligner:

@@ -27,7 +27,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .aligner import DepthAligner
+from .aligner import DepthAligner, check_row_layout
 from .config import RD_SCHEDULER, SD2_UNET, SD2_VAE
 from .scheduler import DDIMScheduler
 from .unet import UNet
@@ -482,7 +482,7 @@ class RollingDepthPipeline:
             out.aligned_snippet_pred_ls = [out.depth_coaligned.float().expand(-1, 3, -1, -1)]
         return out
 
-    def _forward_sharded(self, input_frames, dilations, snippet_lengths, coalign_kwargs, refine_step,
+    def _forward_sharded(self, input_frames, dilations, snippet_lengths, init_infer_steps, coalign_kwargs, refine_step,
                          refine_snippet_len, refine_start_dilation, init_noise, record, generator=None):
         """forward() over W ranks (shard.sharded_forward), outputs assembled on every rank.  Dilations
         arrive already capped (forward's checks ran); the snippets are all-gathered at full
@@ -494,7 +494,8 @@ class RollingDepthPipeline:
         so = sharded_forward(self, input_frames, list(dilations), False, list(snippet_lengths), coalign_kwargs,
                              init_noise=init_noise, group=self._group, refine_step=refine_step,
                              refine_snippet_len=refine_snippet_len, refine_start_dilation=refine_start_dilation,
-                             gather=True, record=record, generator=generator)
+                             gather=True, record=record, generator=generator,
+                             init_infer_steps=list(init_infer_steps))
         snips = gather_rows_by_dilation([r.to(self.dtype) for r in so.snippet_rows], so.snippet_counts, world,
                                         self._group)
         H, W = so.depth_pred_full.shape[-2:]
@@ -538,12 +539,15 @@ class RollingDepthPipeline:
             refine_start_dilation = self.cap_max_dilation(seq_len, refine_snippet_len, refine_start_dilation, verbose)
         if input_frames.shape[0] != 1:
             raise NotImplementedError("Layered inference is only implemented for B=1")
+        # the aligner's row layout / kernel limits, before any inference (the reference fails there
+        # only at its first optimisation step, after all snippets are denoised)
+        check_row_layout(snippet_lengths, int((coalign_kwargs or {}).get("num_iterations", 2000)))
         if self._group is not None:
             import torch.distributed as dist
             if dist.get_world_size(self._group) > 1:
-                return self._forward_sharded(input_frames, dilations, snippet_lengths, coalign_kwargs, refine_step,
-                                             refine_snippet_len, refine_start_dilation, init_noise, record,
-                                             generator)
+                return self._forward_sharded(input_frames, dilations, snippet_lengths, init_infer_steps, coalign_kwargs,
+                                             refine_step, refine_snippet_len, refine_start_dilation, init_noise,
+                                             record, generator)
         # ----------------- encode (H2D boundary :263)
         frames = input_frames[0].to(self.device)
         rgb_latent = self.encode_rgb(frames)

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
+from .config import validate_scheduler_config
 
 
 class DDIMScheduler:
@@ -21,6 +22,7 @@ class DDIMScheduler:
                  beta_schedule: str = "linear", set_alpha_to_one: bool = True, steps_offset: int = 0,
                  prediction_type: str = "epsilon", timestep_spacing: str = "leading",
                  rescale_betas_zero_snr: bool = False, clip_sample: bool = False, **unused):
+        validate_scheduler_config(unused)
         if clip_sample:
             raise NotImplementedError("clip_sample=True is not used by the RollingDepth checkpoints")
         self.config = dict(num_train_timesteps=num_train_timesteps, beta_start=beta_start, beta_end=beta_end,

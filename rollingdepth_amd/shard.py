@@ -181,7 +181,8 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
                     init_noise: Optional[torch.Tensor] = None, group=None, num_frames: Optional[int] = None,
                     to_host: bool = False, refine_step: int = 0, refine_snippet_len: int = 3,
                     refine_start_dilation: int = 6, gather: bool = False, record: Optional[dict] = None,
-                    generator: Optional[torch.Generator] = None) -> ShardedOutput:
+                    generator: Optional[torch.Generator] = None,
+                    init_infer_steps: Union[int, Sequence[int]] = 1) -> ShardedOutput:
     """Multi-GPU RollingDepthPipeline.forward (every preset: refine_step > 0 included).
 
     `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N` —
@@ -191,7 +192,8 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     host memory.  `gather=True` also all-gathers the full depth_pred / depth_coaligned on every rank
     (tests, small N).  `dilations` is not mutated (forward() mutates the caller's list; this is the
     build's own entry point).  `snippet_len`: one length, or one per dilation.  `group` defaults to
-    the world group (refine's all-reduce included).  Without `init_noise` the shared noise is drawn
+    the world group (refine's all-reduce included).  `init_infer_steps`: DDIM steps per snippet, one
+    count or one per dilation (rollingdepth_pipeline.py:421-445), as forward().  Without `init_noise` the shared noise is drawn
     on rank 0 exactly as forward() draws it (from `generator`) and broadcast."""
     from . import kernels as K
     from .aligner import DepthAligner, check_row_layout
@@ -207,6 +209,12 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     slens = [int(x) for x in snippet_len] if isinstance(snippet_len, (list, tuple)) else [int(snippet_len)] * len(dil)
     if len(slens) != len(dil):
         raise ValueError(f"snippet lengths {slens} vs dilations {dil}")
+    steps = [int(x) for x in init_infer_steps] if isinstance(init_infer_steps, (list, tuple)) \
+        else [int(init_infer_steps)] * len(dil)
+    if len(steps) == 1:
+        steps = steps * len(dil)
+    if len(steps) != len(dil) or min(steps) < 1:
+        raise ValueError(f"init_infer_steps {steps} vs dilations {dil} (one count >= 1 per dilation)")
     if cap_dilation:
         dil = [pipe.cap_max_dilation(N, sl, d) for d, sl in zip(dil, slens)]
         refine_start_dilation = pipe.cap_max_dilation(N, refine_snippet_len, refine_start_dilation)
@@ -237,7 +245,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     k0 = [s[0] if s else 0 for s in subsets]
     aligner = DepthAligner(device=dev, **(coalign_kwargs or {}))
     check_row_layout(slens, aligner.num_iterations)
-    rows = pipe.init_snippet_infer(rgb_latent, noise, dil, slens, [1] * len(dil), [1] * len(dil),
+    rows = pipe.init_snippet_infer(rgb_latent, noise, dil, slens, steps, [1] * len(dil),
                                    snippet_subset=subsets)
     H, W = rows[0].shape[-2:]
     d2h = torch.cuda.Stream(dev) if to_host else None

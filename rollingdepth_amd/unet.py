@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import kernels as K
-from .config import unet_heads
+from .config import unet_heads, validate_unet_config
 
 F16, F32 = torch.float16, torch.float32
 
@@ -42,6 +42,10 @@ def _sinusoid(t: int, dim: int, flip: bool, shift: float) -> np.ndarray:
 class _Lin:
     def __init__(self, sd, key, dev, bias=True, dtype=F16):
         w = sd[key + ".weight"]
+        if w.dim() == 4 and tuple(w.shape[2:]) == (1, 1):
+            # Transformer2DModel with use_linear_projection=False (the diffusers default): proj_in /
+            # proj_out are 1×1 convs, the same per-pixel linear map on the NHWC tokens
+            w = w[:, :, 0, 0]
         self.n, self.k = w.shape
         self.w = K.pack_linear(w, dev, dtype)
         self.b = sd[key + ".bias"].to(dev, F32) if bias and key + ".bias" in sd else None
@@ -191,6 +195,7 @@ class UNet:
         dev = torch.device(device)
         if dtype not in (F16, F32):
             raise NotImplementedError(f"UNet storage dtype {dtype} (f16 or f32)")
+        validate_unet_config(cfg)
         self.cfg, self.dev, self.dtype = cfg, dev, dtype
         g, eps = cfg["norm_num_groups"], cfg["norm_eps"]
         heads = unet_heads(cfg)

@@ -18,6 +18,7 @@ from typing import Dict
 import torch
 
 from . import kernels as K
+from .config import validate_vae_config
 from .unet import _Conv, _Lin, _Norm, Resnet
 
 F16, F32 = torch.float16, torch.float32
@@ -64,6 +65,7 @@ class VAE:
         dev = torch.device(device)
         if dtype not in (F16, F32):
             raise NotImplementedError(f"VAE storage dtype {dtype} (f16 or f32)")
+        validate_vae_config(cfg)
         self.cfg, self.dev, self.dtype = cfg, dev, dtype
         g = cfg["norm_num_groups"]
         eps = 1e-6

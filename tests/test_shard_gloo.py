@@ -151,3 +151,75 @@ def test_shard_plan_world2():
 def test_shard_plan_world3():
     """An uneven split (ragged last chunks) — the same plan at W = 3."""
     _run(3)
+
+
+class _StopAtSnippets(Exception):
+    pass
+
+
+class _PlanPipe:
+    """Host-only stand-in for RollingDepthPipeline up to the snippet stage of sharded_forward: records
+    the arguments init_snippet_infer receives on each rank, then stops the forward (the device stages
+    after it are covered by the GPU tests)."""
+
+    def __init__(self):
+        from rollingdepth_amd.pipeline import RollingDepthPipeline
+        from types import SimpleNamespace
+        self.device = torch.device("cpu")
+        self.dtype = torch.float32
+        self.vae = SimpleNamespace(latent_hw=lambda H, W: (H // 8, W // 8), lat_pad=8)
+        self.get_snippet_indice = RollingDepthPipeline.get_snippet_indice
+        self.cap_max_dilation = RollingDepthPipeline.cap_max_dilation
+        self.calls = []
+
+    def encode_rgb(self, frames):
+        return torch.zeros((frames.shape[0], frames.shape[-2] // 8, frames.shape[-1] // 8, 8))
+
+    def _noise_nhwc(self, noise, h, w):
+        return torch.zeros((1, h, w, 8))
+
+    def init_snippet_infer(self, rgb_latent, noise, dilations, snippet_lengths, init_infer_steps, strides,
+                           snippet_subset=None, record=None):
+        self.calls.append(dict(dilations=list(dilations), steps=list(init_infer_steps), subset=snippet_subset))
+        raise _StopAtSnippets
+
+
+def _steps_worker(rank, world, port, res):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rollingdepth_amd.shard import rank_subsets, sharded_forward
+
+    ok = True
+    for steps, want in (([2], [2, 2]), ([1, 3], [1, 3]), (4, [4, 4])):
+        pipe = _PlanPipe()
+        try:
+            sharded_forward(pipe, torch.zeros((1, 30, 3, 16, 16)), [1, 10], True, 3, None,
+                            init_noise=torch.zeros(1, 4, 2, 2), init_infer_steps=steps)
+        except _StopAtSnippets:
+            pass
+        c = pipe.calls[0]
+        counts = [30 - 2 * d for d in c["dilations"]]
+        ok &= c["steps"] == want and c["subset"] == rank_subsets(counts, world, rank)
+    try:  # a count per dilation that does not match the dilations
+        sharded_forward(_PlanPipe(), torch.zeros((1, 30, 3, 16, 16)), [1, 10], True, 3, None,
+                        init_noise=torch.zeros(1, 4, 2, 2), init_infer_steps=[1, 2, 3])
+        ok = False
+    except ValueError:
+        pass
+    res[rank] = int(ok)
+    dist.destroy_process_group()
+
+
+def test_sharded_forward_honours_init_infer_steps_world2():
+    """the sharded forward runs the DDIM step count per dilation that forward() was given
+    (rollingdepth_pipeline.py:421-445), on every rank, with the rank's own snippet subset."""
+    ctx = mp.get_context("spawn")
+    res = ctx.Array("i", [0, 0])
+    port = _free_port()
+    procs = [ctx.Process(target=_steps_worker, args=(r, 2, port, res)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    assert list(res) == [1, 1]
