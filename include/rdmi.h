@@ -238,7 +238,8 @@ int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* 
                       long P, int C, int Cpad, float ca, float cb, float out_scale, long e_period,
                       int dtype, void* stream);
 /* Refine averaging (rollingdepth_pipeline.py:586-629): out[f] = mean over the snippets s = f − j·stride
- * (0 ≤ s < n) of src[s][j]; src [n][w][P][ld], out [N][P][ld] f16 (channels ≥ C zeroed). */
+ * (0 ≤ s < n) of src[s][j]; src [n][w][P][ld], out [N][P][ld] f16 (channels ≥ C zeroed).  The sum is
+ * taken in f64 (exact for these few f32 terms, hence independent of the order of addition). */
 int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld,
                          void* out, int dtype, void* stream);
 /* Depth colourisation (src/util/colorize.py:12-93, the CLI's visualisation): rgb [n][3] u8 =
@@ -249,14 +250,15 @@ int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long 
  * write the table index per pixel instead (lut / rgb unused). */
 int rdmi_colorize(const void* depth, int dtype, long n, const void* minmax, const unsigned char* lut, int lut_n,
                   unsigned char* rgb, int* index, void* stream);
-/* Sharded refine averaging (the loop above split over ranks): sum [N][P][C] f32 =
+/* Sharded refine averaging (the loop above split over ranks): sum [N][P][C] f64 =
  * per frame the sum over THIS rank's snippets k0 .. k0+nloc-1 (src [nloc][w][P][ld], dtype RDMI_F16 /
  * RDMI_F32), zero where none covers the frame; after an all-reduce SUM over ranks,
  * rdmi_snippet_finish divides by the frame's cover count over all n snippets → out [N][P][ld]
- * (channels ≥ C zeroed).  World size 1 reproduces rdmi_snippet_average bitwise. */
+ * (channels ≥ C zeroed).  The f64 sums are exact, so every world size and every all-reduce order
+ * reproduces rdmi_snippet_average bitwise. */
 int rdmi_snippet_accumulate(const void* src, int dtype, int k0, int nloc, int w, int stride, int N, long P, int C,
-                            int ld, float* sum, void* stream);
-int rdmi_snippet_finish(const float* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
+                            int ld, double* sum, void* stream);
+int rdmi_snippet_finish(const double* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
                         int dtype, void* stream);
 /* Global min/max of an f16 or f32 buffer → minmax[2] f32 (workspace ≥ 2*1024 floats)
  * (the `min([snippet.min() ...])` of depth_aligner.py:78 and the min/max of :316-317). */
@@ -304,16 +306,17 @@ int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float*
                        long HW, const float* shift, float* out, void* stream);
 
 /* Sharded merge: each rank sums s·x+t of ITS full-resolution snippets — rows
- * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w_d][HW] — into sum_out [seq_len][HW] f32 (the
+ * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w_d][HW] — into sum_out [seq_len][HW] f64 (the
  * same per-slot arithmetic as rdmi_aligner_merge, zero where no local slot covers a frame); after a
  * reduce-scatter SUM by frame, rdmi_aligner_merge_finish divides frames f0 .. f0+nf-1 by their cover
- * count over all n[d] snippets.  World size 1 reproduces rdmi_aligner_merge bitwise. */
+ * count over all n[d] snippets.  With f32 arithmetic (x_f32 1 / 2) the f64 sums are exact, so any world
+ * size and reduction order reproduces rdmi_aligner_merge bitwise. */
 int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                const float* const* t, const int* n, const int* stride, const int* k0,
-                               const int* nloc, const int* w, int seq_len, long HW, const float* shift, float* sum_out,
+                               const int* nloc, const int* w, int seq_len, long HW, const float* shift, double* sum_out,
                                void* stream);
 int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf, long HW,
-                              const float* sum, float* out, void* stream);
+                              const double* sum, float* out, void* stream);
 
 /* Single-head flash attention for head dim 512 (f16): the VAE mid-block attention
  * (unet_2d_blocks.py:680-697 through AttnProcessor2_0's 4-D path, attention_processor.py:2172-2276 —

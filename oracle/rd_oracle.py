@@ -488,8 +488,8 @@ def decode_depth(sd, vcfg, lat: torch.Tensor, max_bs=4) -> torch.Tensor:
 
 
 def snippet_denoise(usd, ucfg, sched: DDIM, rgb_lat, init_noise, idx_list, context, steps=1):
-    """init_snippet_infer inner loop (:415-446) for one dilation: per snippet gather, 1-step
-    UNet (rgb latent first in the 8-channel input, :650-651) + DDIM step."""
+    """init_snippet_infer inner loop (:415-446) for one dilation: per snippet gather, then `steps`
+    UNet (rgb latent first in the 8-channel input, :650-651) + DDIM steps over the set timesteps."""
     outs = []
     for ids in idx_list:
         r = rgb_lat[ids]
@@ -530,15 +530,18 @@ def refine(usd, ucfg, sched: DDIM, rgb_lat, depth_lat, init_noise, refine_step, 
 def pipeline_forward(usd, ucfg, vsd, vcfg, scfg, frames: torch.Tensor, init_noise: torch.Tensor,
                      context: torch.Tensor, dilations: List[int], cap_dilation=True, snippet_len=3,
                      coalign_kwargs=None, max_vae_bs=4, record=None, refine_step=0, refine_snippet_len=3,
-                     refine_start_dilation=6):
+                     refine_start_dilation=6, init_infer_steps=(1,)):
     """RollingDepthPipeline.forward (rollingdepth_pipeline.py:193-354), stride 1.
     frames [N,3,H,W] in [-1,1]; init_noise [1,4,h,w] (broadcast to all frames, :282-288).
-    snippet_len: one length or one per dilation (:215-226)."""
+    snippet_len: one length or one per dilation (:215-226); init_infer_steps likewise (:227-231)."""
     N = frames.shape[0]
     dil = list(dilations)
     slens = list(snippet_len) if isinstance(snippet_len, (list, tuple)) else [snippet_len]
     if len(slens) == 1:
         slens = slens * len(dil)  # rollingdepth_pipeline.py:220-223
+    steps = list(init_infer_steps)
+    if len(steps) == 1:
+        steps = steps * len(dil)  # rollingdepth_pipeline.py:227-231
     if cap_dilation:
         dil = [cap_max_dilation(N, sl, d) for d, sl in zip(dil, slens)]
         refine_start_dilation = cap_max_dilation(N, refine_snippet_len, refine_start_dilation)
@@ -546,9 +549,9 @@ def pipeline_forward(usd, ucfg, vsd, vcfg, scfg, frames: torch.Tensor, init_nois
     noise = init_noise.expand(N, *init_noise.shape[1:])
     sched = DDIM(scfg)
     snippets = []
-    for d, sl in zip(dil, slens):
+    for d, sl, ns in zip(dil, slens, steps):
         ids = snippet_indices(0, 1, N, sl, d, d)
-        lat = snippet_denoise(usd, ucfg, sched, rgb_lat, noise, ids, context)
+        lat = snippet_denoise(usd, ucfg, sched, rgb_lat, noise, ids, context, ns)
         nd, w = lat.shape[:2]
         dec = decode_depth(vsd, vcfg, lat.reshape(nd * w, *lat.shape[2:]), max_vae_bs)
         snippets.append(dec.reshape(nd, w, 1, *dec.shape[-2:]))

@@ -428,11 +428,12 @@ struct MergeP {
   int n[MAXD], stride[MAXD], w[MAXD];
   int k0[MAXD], nloc[MAXD];  // rows of x[d] are global snippets k0[d] .. k0[d]+nloc[d]-1
   int nd, xf32;
-  int sum_only;              // 1: write the per-frame sum (sharded merge), 0: the mean
+  int sum_only;              // 1: write the per-frame f64 sum (sharded merge) to dsum, 0: the mean to out
   int f0;                    // first frame of out (out rows are frames f0 .. f0+gridDim.y-1)
   long HW;
   const float* shift;
   float* out;
+  double* dsum;
 };
 
 // number of (dilation, slot) pairs covering frame f (the B.sum(0) of depth_aligner.py:190 / the
@@ -447,11 +448,17 @@ __device__ __forceinline__ int cover_count(const int* n, const int* stride, int 
   return cnt;
 }
 
+// The f32-arithmetic merges (x_f32 1 / 2) add the slots' f32 terms s·x + t in f64: the sum of a
+// frame's few (≤ Σ w_d) f32 terms is then exact, so it does not depend on the order the terms are
+// added in — the sharded merge (per-rank partial sums, reduce-scatter in RCCL's order, finish)
+// gives bitwise the single-GPU result, and both round once, at the mean.  The f16-emulating mode 0
+// (the reference's fp16 merge, RDMI_MERGE_F32=0) keeps its f32 running sum.
 __global__ void merge_k(MergeP p) {
   const int f = p.f0 + blockIdx.y;
   const float sh = p.shift ? p.shift[0] : 0.f;
   for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
     float sum = 0.f;
+    double dsum = 0.0;
     int cnt = 0;
     for (int d = 0; d < p.nd; ++d) {
       for (int j = p.w[d] - 1; j >= 0; --j) {  // boolean-mask order over [n_d, w]: k ascending
@@ -471,22 +478,29 @@ __global__ void merge_k(MergeP p) {
           f16 prod = (f16)((float)xs * (float)sc);
           a = (float)(f16)((float)prod + (float)tr);
         }
-        sum = addrn(sum, a);
+        if (p.xf32)
+          dsum += (double)a;
+        else
+          sum = addrn(sum, a);
         ++cnt;
       }
     }
-    p.out[(long)blockIdx.y * p.HW + px] = p.sum_only ? sum : (cnt ? sum / (float)cnt : 0.f);
+    const long o = (long)blockIdx.y * p.HW + px;
+    if (p.sum_only)
+      p.dsum[o] = p.xf32 ? dsum : (double)sum;
+    else
+      p.out[o] = p.xf32 ? (cnt ? (float)(dsum / (double)cnt) : 0.f) : (cnt ? sum / (float)cnt : 0.f);
   }
 }
 
 // sharded merge, second half: out[f] = sum[f] / (number of covering slots of frame f0 + f over ALL
 // snippets), after the per-rank sums were reduced over ranks
-__global__ void merge_finish_k(MergeP p, const float* __restrict__ sum) {
+__global__ void merge_finish_k(MergeP p, const double* __restrict__ sum) {
   const int fl = blockIdx.y;
   const int cnt = cover_count(p.n, p.stride, p.nd, p.w, p.f0 + fl);
   for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
     const long i = (long)fl * p.HW + px;
-    p.out[i] = cnt ? sum[i] / (float)cnt : 0.f;
+    p.out[i] = cnt ? (float)(sum[i] / (double)cnt) : 0.f;
   }
 }
 
@@ -646,8 +660,8 @@ extern "C" int rdmi_aligner_prepare(const void* x, int x_f32, int n, int w, int 
 
 static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float* const* s, const float* const* t,
                         const int* n, const int* stride, const int* k0, const int* nloc, const int* w, int f0, int nf,
-                        long HW, const float* shift, float* out, int sum_only, void* stream) {
-  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && out && HW > 0 && nf >= 0 && f0 >= 0, RDMI_E_ARG,
+                        long HW, const float* shift, float* out, double* dsum, void* stream) {
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && (out || dsum) && HW > 0 && nf >= 0 && f0 >= 0, RDMI_E_ARG,
                "aligner_merge: bad args");
   MergeP p{};
   for (int d = 0; d < n_dil; ++d) {
@@ -663,8 +677,8 @@ static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float
     p.nloc[d] = nl;
     p.w[d] = w[d];
   }
-  p.nd = n_dil; p.xf32 = x_f32; p.HW = HW; p.shift = shift; p.out = out;
-  p.sum_only = sum_only; p.f0 = f0;
+  p.nd = n_dil; p.xf32 = x_f32; p.HW = HW; p.shift = shift; p.out = out; p.dsum = dsum;
+  p.sum_only = dsum != nullptr; p.f0 = f0;
   if (nf == 0) return 0;
   long gx = (HW + 255) / 256;
   if (gx > 1024) gx = 1024;
@@ -675,19 +689,21 @@ static int merge_launch(int n_dil, const void* const* xf, int x_f32, const float
 extern "C" int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                   const float* const* t, const int* n, const int* stride, const int* w, int seq_len, long HW,
                                   const float* shift, float* out, void* stream) {
-  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, nullptr, nullptr, w, 0, seq_len, HW, shift, out, 0, stream);
+  RDMI_REQUIRE(out, RDMI_E_ARG, "aligner_merge: null out");
+  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, nullptr, nullptr, w, 0, seq_len, HW, shift, out, nullptr,
+                      stream);
 }
 
 extern "C" int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                           const float* const* t, const int* n, const int* stride, const int* k0,
                                           const int* nloc, const int* w, int seq_len, long HW, const float* shift,
-                                          float* sum_out, void* stream) {
-  RDMI_REQUIRE(k0 && nloc, RDMI_E_ARG, "aligner_merge_partial: k0/nloc required");
-  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, 0, seq_len, HW, shift, sum_out, 1, stream);
+                                          double* sum_out, void* stream) {
+  RDMI_REQUIRE(k0 && nloc && sum_out, RDMI_E_ARG, "aligner_merge_partial: k0/nloc/sum_out required");
+  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, 0, seq_len, HW, shift, nullptr, sum_out, stream);
 }
 
 extern "C" int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf,
-                                         long HW, const float* sum, float* out, void* stream) {
+                                         long HW, const double* sum, float* out, void* stream) {
   RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && sum && out && HW > 0 && f0 >= 0 && nf >= 0,
                RDMI_E_ARG, "aligner_merge_finish: bad args");
   if (nf == 0) return 0;

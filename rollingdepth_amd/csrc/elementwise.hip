@@ -135,15 +135,17 @@ __global__ void snippet_average_k(const T* __restrict__ src, int n, int w, int s
     const int c = (int)(i % ld);
     float v = 0.f;
     if (c < C) {
-      float s = 0.f;
+      // f64 sum of the ≤ w covering predictions: exact, so the sharded refine's per-rank sums
+      // (snippet_accumulate_k, all-reduced in any order, snippet_finish_k) reproduce it bitwise
+      double s = 0.0;
       int cnt = 0;
       for (int j = w - 1; j >= 0; --j) {  // snippet index ascending
         const int sn = f - j * stride;
         if (sn < 0 || sn >= n) continue;
-        s += (float)src[((long)sn * w + j) * tot + i];
+        s += (double)(float)src[((long)sn * w + j) * tot + i];
         ++cnt;
       }
-      v = cnt ? s / (float)cnt : 0.f;
+      v = cnt ? (float)(s / (double)cnt) : 0.f;
     }
     out[(long)f * tot + i] = (T)v;
   }
@@ -154,24 +156,24 @@ __global__ void snippet_average_k(const T* __restrict__ src, int n, int w, int s
 // frames (zeros where no local snippet covers f) — all-reduced over ranks, then snippet_finish_k
 template <typename T>
 __global__ void snippet_accumulate_k(const T* __restrict__ src, int k0, int nloc, int w, int stride, long P, int C,
-                                     int ld, float* __restrict__ sum) {
+                                     int ld, double* __restrict__ sum) {
   const int f = blockIdx.y;
   const long tot = P * C;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
     const long p = i / C;
     const int c = (int)(i - p * C);
-    float s = 0.f;
+    double s = 0.0;
     for (int j = w - 1; j >= 0; --j) {
       const int sn = f - j * stride;
       if (sn < k0 || sn >= k0 + nloc) continue;
-      s += (float)src[((long)(sn - k0) * w + j) * P * ld + p * ld + c];
+      s += (double)(float)src[((long)(sn - k0) * w + j) * P * ld + p * ld + c];
     }
     sum[(long)f * tot + i] = s;
   }
 }
 
 template <typename T>
-__global__ void snippet_finish_k(const float* __restrict__ sum, int n, int w, int stride, long P, int C, int ld,
+__global__ void snippet_finish_k(const double* __restrict__ sum, int n, int w, int stride, long P, int C, int ld,
                                  T* __restrict__ out) {
   const int f = blockIdx.y;
   int cnt = 0;
@@ -184,7 +186,7 @@ __global__ void snippet_finish_k(const float* __restrict__ sum, int n, int w, in
     const long p = i / ld;
     const int c = (int)(i - p * ld);
     float v = 0.f;
-    if (c < C && cnt) v = sum[((long)f * P + p) * C + c] / (float)cnt;
+    if (c < C && cnt) v = (float)(sum[((long)f * P + p) * C + c] / (double)cnt);
     out[(long)f * tot + i] = (T)v;
   }
 }
@@ -414,7 +416,7 @@ extern "C" int rdmi_snippet_average(const void* src, int n, int w, int stride, i
 }
 
 extern "C" int rdmi_snippet_accumulate(const void* src, int dtype, int k0, int nloc, int w, int stride, int N, long P,
-                                       int C, int ld, float* sum, void* stream) {
+                                       int C, int ld, double* sum, void* stream) {
   RDMI_REQUIRE(sum && N > 0 && w > 0 && ld >= C && k0 >= 0 && nloc >= 0 && (nloc == 0 || src), RDMI_E_ARG,
                "snippet_accumulate: bad args");
   long gx = (P * C + 255) / 256;
@@ -428,7 +430,7 @@ extern "C" int rdmi_snippet_accumulate(const void* src, int dtype, int k0, int n
   return rdmi::check_launch("snippet_accumulate");
 }
 
-extern "C" int rdmi_snippet_finish(const float* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
+extern "C" int rdmi_snippet_finish(const double* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
                                    int dtype, void* stream) {
   RDMI_REQUIRE(sum && out && n > 0 && w > 0 && N > 0 && ld >= C, RDMI_E_ARG, "snippet_finish: bad args");
   long gx = (P * ld + 255) / 256;

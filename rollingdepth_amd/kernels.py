@@ -770,18 +770,21 @@ def _dtype_code(t: torch.Tensor) -> int:
 def snippet_accumulate(src: torch.Tensor, k0: int, stride: int, N: int, c: int = 4,
                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sharded refine, rank-local half: src [nloc, w, h, wd, ld] (global snippets k0 .. k0+nloc-1) →
-    f32 [N, h·wd, c] per-frame sums over the local snippets (zeros elsewhere)."""
+    f64 [N, h·wd, c] per-frame sums over the local snippets (zeros elsewhere; exact sums, so the
+    all-reduce order does not change the averages)."""
     nloc, w, h, wd, ld = src.shape
     src = src.contiguous()
-    out = torch.empty((N, h * wd, c), dtype=F32, device=src.device) if out is None else out
+    out = torch.empty((N, h * wd, c), dtype=torch.float64, device=src.device) if out is None else out
     check(lib.rdmi_snippet_accumulate(src.data_ptr() if nloc else None, _dtype_code(src), k0, nloc, w, stride, N,
                                       h * wd, c, ld, out.data_ptr(), _stream()), "rdmi_snippet_accumulate")
     return out
 
 
 def snippet_finish(sums: torch.Tensor, n: int, w: int, stride: int, hw, ld: int, dtype=F16) -> torch.Tensor:
-    """Sharded refine, after the all-reduce: f32 [N, P, c] sums → [N, h, wd, ld] means (÷ the frame's
+    """Sharded refine, after the all-reduce: f64 [N, P, c] sums → [N, h, wd, ld] means (÷ the frame's
     cover count over all n snippets)."""
+    if sums.dtype != torch.float64:
+        raise TypeError("snippet_finish: f64 sums expected (snippet_accumulate)")
     N, P, c = sums.shape
     h, wd = hw
     out = torch.empty((N, h, wd, ld), dtype=dtype, device=sums.device)
@@ -867,10 +870,11 @@ def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int
                           strides, w: Sequence[int], seq_len: int, HW: int, shift: torch.Tensor, x_f32,
                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Sharded merge, rank-local half: xf[d] [nloc_d, w_d, H, W] = global snippets k0[d] .. of dilation
-    d (None / 0 rows when the rank owns none) → f32 [seq_len, HW] per-frame sums of s·x+t."""
+    d (None / 0 rows when the rank owns none) → f64 [seq_len, HW] per-frame sums of s·x+t (exact in
+    the f32-arithmetic modes, so the reduce-scatter order does not change the merged map)."""
     nd = len(xf)
     wv = (C.c_int * nd)(*list(w))
-    out = torch.empty((seq_len, HW), dtype=F32, device=shift.device) if out is None else out
+    out = torch.empty((seq_len, HW), dtype=torch.float64, device=shift.device) if out is None else out
     xp = (C.c_void_p * nd)(*[(x.data_ptr() if x is not None and x.shape[0] else None) for x in xf])
     sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
     tp = (C.c_void_p * nd)(*[t.data_ptr() for t in trans])
@@ -885,11 +889,13 @@ def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int
 
 def aligner_merge_finish(sums: torch.Tensor, n: Sequence[int], strides: Sequence[int], w: Sequence[int],
                          f0: int) -> torch.Tensor:
-    """Sharded merge, after the reduce-scatter: f32 [nf, HW] sums of frames f0 .. → per-frame means
+    """Sharded merge, after the reduce-scatter: f64 [nf, HW] sums of frames f0 .. → f32 per-frame means
     (w: snippet length per dilation)."""
+    if sums.dtype != torch.float64:
+        raise TypeError("aligner_merge_finish: f64 sums expected (aligner_merge_partial)")
     nf, HW = sums.shape
     nd = len(n)
-    out = torch.empty_like(sums)
+    out = torch.empty((nf, HW), dtype=F32, device=sums.device)
     nn = (C.c_int * nd)(*list(n))
     stv = (C.c_int * nd)(*list(strides))
     wv = (C.c_int * nd)(*list(w))

@@ -362,13 +362,14 @@ class RollingDepthPipeline:
                 for si, t in enumerate(timesteps.tolist()):
                     pred = self.unet.forward(x, int(t), num_view=slen)
                     last = si == len(timesteps) - 1
+                    if record is not None:  # every UNet call (the reference's single_step outputs)
+                        record.setdefault("unet_out", []).append(pred)
                     if last:
                         zin = self.scheduler.step_(pred, int(t), depth_view, 1.0 / self.depth_latent_scale_factor,
                                                    channels=self.N_CHANNEL_PER_LATENT,
                                                    out=torch.empty((x.shape[0], h, w, 8), dtype=self.dtype,
                                                                    device=self.device))
                         if record is not None:
-                            record.setdefault("unet_out", []).append(pred)
                             record.setdefault("snippet_latent", []).append(
                                 self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4,
                                                      out=torch.empty((x.shape[0], h, w, 8), dtype=self.dtype,

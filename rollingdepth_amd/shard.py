@@ -23,11 +23,15 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Per f
 Outputs stay distributed: rank r holds depth / coaligned depth for frames chunk_bounds(N, W)[r]
 (and its own decoded snippets); `gather=True` assembles the full maps on every rank.
 
-Numerics vs the single-GPU forward: identical per-snippet arithmetic, but not bitwise — the kernel
-engine chosen per launch depends on the batch shape (f32 accumulation order), the merge / refine sums
-are reduced across ranks in RCCL's order, and the aligner runs on the same inputs but the snippets
-each rank batched differ.  Stated tolerance: depth mean |Δ| ≤ 1e-3 (the north_star bound) against
-the single-GPU result (tests/test_pipeline_gpu.py); with W = 1 the plan reproduces forward bitwise.
+Numerics vs the single-GPU forward: identical per-snippet arithmetic.  The cross-rank sums — the
+merge of s·x+t per frame and refine's per-frame average of snippet predictions — are exact f64 sums
+of f32 terms on both paths (aligner.hip merge_k, elementwise.hip snippet_*), so the order RCCL
+reduces them in does not change a bit; the aligner runs the same kernel on the same (all-gathered)
+inputs.  What can still differ is the kernel engine chosen per launch shape (the f32 accumulation
+order inside a conv / GEMM depends on the batch a rank runs), which at SD2 shapes is not bitwise.
+Stated tolerance: depth mean |Δ| ≤ 1e-3 (the north_star bound) against the single-GPU result
+(tests/test_pipeline_gpu.py); at the test sizes the sharded forward, refine included, reproduces the
+single-GPU forward bitwise.
 """
 from __future__ import annotations
 
@@ -268,7 +272,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     sums = K.aligner_merge_partial([r if r.shape[0] else None for r in rows], k0, counts, scales, trans, strides,
                                    slens, N, H * W, shift, x_f32=1 if rows_f32 else (2 if pipe.merge_f32 else 0))
     my_sums = _reduce_scatter_rows(sums, world, group)
-    merged = K.aligner_merge_finish(my_sums, counts, strides, slens, f0) if f1 > f0 else my_sums
+    merged = K.aligner_merge_finish(my_sums, counts, strides, slens, f0) if f1 > f0 else my_sums.float()
     # merge_scaled_triplets returns the snippets' dtype (unless the pipeline merges in f32)
     d = (merged if (pipe.merge_f32 or rows_f32) else merged.to(pipe.dtype).float()).contiguous()
     mm_d = K.minmax(d) if d.numel() else torch.tensor([float("inf"), float("-inf")], device=dev)

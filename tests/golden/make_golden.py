@@ -17,6 +17,8 @@ Fixtures (all inputs synthesised deterministically, rollingdepth_amd/weights.py)
   aligner_mixed.safetensors (+ .json)       DepthAligner.run with snippet lengths [3, 2] (rows of the
                                             two dilations coincide: the reference's overwrite)
   tiny_mixed.safetensors (+ .json)          RollingDepthPipeline.forward, tiny, snippet_lengths [3, 2]
+  tiny_steps2 / tiny_steps13 (+ .json)      RollingDepthPipeline.forward, tiny, init_infer_steps [2] and
+                                            [1, 3] (per dilation): multi-step DDIM per snippet
   sd2_768_f32.safetensors (+ .json)         the sd2_768 run stored in f32 (paper-preset precision)
   ddim.json                                 DDIMScheduler timesteps / step / add_noise values
   snippet_indices.json                      get_snippet_indice / cap_max_dilation / aligner indices
@@ -58,7 +60,7 @@ def build_pipe(P, ucfg, vcfg, scfg, seed=0):
 
 
 def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step=0, refine_start=6,
-             snippet_lengths=(3,)):
+             snippet_lengths=(3,), init_infer_steps=(1,)):
     rec = {"unet_out": [], "snip_lat": []}
     orig_single = pipe.single_step
     orig_dec = pipe.decode_depth
@@ -86,7 +88,7 @@ def run_pipe(pipe, frames, dilations, cap, noise_seed, coalign=None, refine_step
     with torch.no_grad():
         out = pipe.forward(
             input_frames=frames[None], dilations=dil, cap_dilation=cap, snippet_lengths=list(snippet_lengths),
-            init_infer_steps=[1], strides=[1], coalign_kwargs=coalign, refine_step=refine_step,
+            init_infer_steps=list(init_infer_steps), strides=[1], coalign_kwargs=coalign, refine_step=refine_step,
             refine_snippet_len=3, refine_start_dilation=refine_start, generator=g, verbose=False,
             max_vae_bs=4, unload_snippet=False)
     rec["dilations_used"] = dil  # forward mutates the caller's list in place (:246-252)
@@ -124,13 +126,14 @@ def attach_clip(P, pipe):
 
 
 def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, refine_step=0, refine_start=6,
-                     clip=False, snippet_lengths=(3,)):
+                     clip=False, snippet_lengths=(3,), init_infer_steps=(1,)):
     pipe = build_pipe(P, ucfg, vcfg, C.RD_SCHEDULER)
     if clip:
         attach_clip(P, pipe)
     h, w = frames.shape[-2] // C.vae_downscale(vcfg), frames.shape[-1] // C.vae_downscale(vcfg)
     noise = torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(1))
-    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign, refine_step, refine_start, snippet_lengths)
+    out, rec = run_pipe(pipe, frames, dilations, cap, 1, coalign, refine_step, refine_start, snippet_lengths,
+                        init_infer_steps)
     t = {
         "frames": _c(frames), "init_noise": _c(noise), "context": _c(pipe.empty_text_embed),
         "rgb_latent": rec["rgb_latent"], "depth_pred": _c(out.depth_pred),
@@ -146,7 +149,8 @@ def pipeline_fixture(P, name, ucfg, vcfg, frames, dilations, cap, coalign=None, 
     meta = {"dilations_in": list(dilations), "dilations_used": rec["dilations_used"], "cap_dilation": cap,
             "unet": ucfg, "vae": vcfg, "scheduler": C.RD_SCHEDULER, "coalign": coalign or {},
             "refine_step": refine_step, "refine_start_dilation": refine_start,
-            "snippet_lengths": list(snippet_lengths)}
+            "snippet_lengths": list(snippet_lengths), "init_infer_steps": list(init_infer_steps),
+            "n_unet_calls": len(rec["unet_out"])}
     if clip:  # the context above is the reference's encode_empty_text output
         meta.update(text_encoder=TINY_CLIP, tokenizer_vocab=TINY_VOCAB, text_encoder_seed=0)
     json.dump(meta, open(os.path.join(HERE, name + ".json"), "w"), indent=1)
@@ -356,7 +360,7 @@ def main():
     torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", os.cpu_count() or 8)))
     P, A = _refload.load_reference()
     todo = a.only.split(",") if a.only else ["keys", "idx", "ddim", "attn", "aligner", "aligner_mixed", "tiny",
-                                             "tiny_mixed", "refine", "clip", "colorize", "sd2"]
+                                             "tiny_mixed", "refine", "clip", "colorize", "sd2", "steps"]
     if "keys" in todo:
         keys_fixture()
     if "idx" in todo:
@@ -379,6 +383,11 @@ def main():
     if "tiny_mixed" in todo:  # snippet_lengths [3, 2] (rollingdepth_pipeline.py:221-226)
         frames = W.synth_frames(9, 32, 32, seed=0)
         pipeline_fixture(P, "tiny_mixed", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, snippet_lengths=(3, 2))
+    if "steps" in todo:  # init_infer_steps > 1: each snippet denoised over several DDIM steps
+        # (rollingdepth_pipeline.py:421-445; scheduling_ddim.py:342-468, prev_timestep = t - T/n)
+        frames = W.synth_frames(9, 32, 32, seed=0)
+        pipeline_fixture(P, "tiny_steps2", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, init_infer_steps=(2,))
+        pipeline_fixture(P, "tiny_steps13", C.TINY_UNET, C.TINY_VAE, frames, [1, 3], True, init_infer_steps=(1, 3))
     if "colorize" in todo:
         colorize_fixture()
     if "clip" in todo:  # tiny pipeline whose empty-text context comes from the reference's CLIP path

@@ -115,7 +115,8 @@ def _pipeline_check(name, tol_lat, tol_depth):
                                meta["dilations_in"], meta["cap_dilation"], coalign_kwargs=meta["coalign"], record=rec,
                                refine_step=meta.get("refine_step", 0),
                                refine_start_dilation=meta.get("refine_start_dilation", 6),
-                               snippet_len=meta.get("snippet_lengths", [3]))
+                               snippet_len=meta.get("snippet_lengths", [3]),
+                               init_infer_steps=meta.get("init_infer_steps", [1]))
     assert rec["dilations"] == meta["dilations_used"]
     torch.testing.assert_close(rec["rgb_latent"], t["rgb_latent"], rtol=0, atol=tol_lat)
     for i in range(len(rec["snippets"])):
@@ -139,6 +140,13 @@ def test_tiny_pipeline_oracle_vs_reference():
 def test_tiny_mixed_lengths_oracle_vs_reference():
     """snippet_lengths [3, 2] (rollingdepth_pipeline.py:215-226) through the whole forward."""
     _pipeline_check("tiny_mixed", 1e-4, 1e-3)
+
+
+@pytest.mark.parametrize("name", ["tiny_steps2", "tiny_steps13"])
+def test_multistep_denoise_oracle_vs_reference(name):
+    """init_infer_steps [2] and [1, 3] (rollingdepth_pipeline.py:421-445): several DDIM steps per
+    snippet, timesteps and prev_timestep as scheduling_ddim.py:297-340 / :342-468 set them."""
+    _pipeline_check(name, 1e-4, 1e-3)
 
 
 def test_aligner_row_overflow_raises_like_reference():

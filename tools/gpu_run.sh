@@ -4,7 +4,7 @@
 #   TAG=r04a STEPS="tests smoke bench shapes prof" bash tools/gpu_run.sh
 #
 # Steps, run in the order given, each under its own time limit, output in gpurun_out/${TAG}_<step>.*:
-#   tests    pytest -m gpu (TEST_SEL narrows it, TEST_ARGS adds options)
+#   tests    pytest -m gpu (TEST_K: a -k expression, TEST_SEL: test paths, TEST_ARGS: more options)
 #   smoke    __graft_entry__.smoke()
 #   bench    bench.py ${BENCH_ARGS} (default preset, --steps ${BENCH_STEPS:-3} --warmup 2)
 #   shapes   one step with RDMI_PROF_SHAPES=1 (per-launch-shape TF/s table in the JSON line)
@@ -24,8 +24,8 @@ hb() { bash tools/hb.sh "$@"; }
 for s in $STEPS; do
   case $s in
     tests)
-      hb timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -q ${TEST_ARGS:---maxfail=20} \
-        --timeout 300 --timeout-method thread ${TEST_SEL:-} > gpurun_out/${TAG}_gpu_tests.log 2>&1; rc=$? ;;
+      hb timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TEST_SEL:-tests} -m gpu -q ${TEST_ARGS:---maxfail=20} \
+        --timeout 300 --timeout-method thread ${TEST_K:+-k "$TEST_K"} > gpurun_out/${TAG}_gpu_tests.log 2>&1; rc=$? ;;
     smoke)
       hb timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1; rc=$? ;;
     bench)
