@@ -145,11 +145,12 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     voff[i] = (unsigned)(row * p.v_ld + vchunk * 8) * 2u;
   }
   const unsigned kstep = (unsigned)(KB * p.k_ld * 2), vstep = (unsigned)(KB * p.v_ld * 2);
+  const int wids = __builtin_amdgcn_readfirstlane(wid);  // provably uniform: the LDS-DMA destinations in SGPRs
   auto issue = [&](int kt) {
     const int slot = kt % NSLOT;
 #pragma unroll
     for (int i = 0; i < DPW; ++i) {
-      f16* ks_ = lds + slot * 2 * TILE + (i * NWV + wid) * 8 * 64;
+      f16* ks_ = lds + slot * 2 * TILE + (i * NWV + wids) * 8 * 64;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)ks_, 16,
                                                koff[i] + (unsigned)kt * kstep, 0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(ks_ + TILE), 16,
