@@ -35,6 +35,9 @@ def conv_cases():
         ("unet L1 640->640 48^2 x24", 24, 48, 48, 640, 640, False),
         ("unet L2 1280->1280 24^2 x24", 24, 24, 24, 1280, 1280, False),
         ("unet L3 1280->1280 12^2 x24", 24, 12, 12, 1280, 1280, False),
+        # the pipeline's UNet launch shape: a 25-snippet batch = 75 frames (pipeline._snippet_batches)
+        ("unet L2 1280->1280 24^2 x75", 75, 24, 24, 1280, 1280, False),
+        ("unet L3 1280->1280 12^2 x75", 75, 12, 12, 1280, 1280, False),
         ("unet up 960->320 96^2 x24", 24, 96, 96, 960, 320, False),
         ("vae 512->512 96^2 x8", 8, 96, 96, 512, 512, False),
         ("vae 512->512 192^2 x8", 8, 192, 192, 512, 512, False),
@@ -123,6 +126,8 @@ def bench_gemm(iters):
     for lab, M, N, Kd, geglu in [("L0 qkv 221k x 960 x 320", 221184, 960, 320, False),
                                  ("L0 ff1 geglu 221k x 2560 x 320", 221184, 2560, 320, True),
                                  ("L0 proj 221k x 320 x 320 +res", 221184, 320, 320, False),
+                                 ("L0 proj 691k x 320 x 320 +res (x75)", 691200, 320, 320, False),
+                                 ("L0 qkv 691k x 960 x 320 (x75)", 691200, 960, 320, False),
                                  ("L1 proj 55k x 640 x 640 +res", 55296, 640, 640, False),
                                  ("L1 ff1 geglu 55k x 5120 x 640", 55296, 5120, 640, True),
                                  ("L0 ff2 221k x 320 x 1280", 221184, 320, 1280, False),
