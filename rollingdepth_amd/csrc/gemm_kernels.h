@@ -180,6 +180,7 @@ struct LinRows {
   __device__ long slot(int i) const { return (mw + (i - 1) * 16) >> 5; }
   __device__ bool full(int n) const { return mw + n * 16 <= M; }
   __device__ int group(int n, int rpg) const { return mw / rpg == (mw + n * 16 - 1) / rpg ? mw / rpg : -1; }
+  __device__ int rstep() const { return 16; }  // row(i + 1) - row(i) where full()
 };
 struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; Ho even, Wo % 16 == 0
   int b, Ho, Wo, y0, x0, rw, fr;
@@ -187,6 +188,7 @@ struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; H
   __device__ long slot(int i) const { return (long)((b * Ho + y0 + rw + i - 1) >> 1) * (Wo >> 4) + (x0 >> 4); }
   __device__ bool full(int) const { return true; }
   __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }  // conv: rpg = Ho·Wo
+  __device__ int rstep() const { return Wo; }
 };
 // Output phase (a, c) of a ×2-upsampled conv computed on the source grid (conv_halo_kernel MODE 3):
 // phase-grid patch rows y0 + rw + i, columns x0 + fr → output pixel (2y + a, 2x + c) of the
@@ -200,6 +202,7 @@ struct PhaseRows {
   }
   __device__ bool full(int) const { return true; }
   __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }
+  __device__ int rstep() const { return 2 * Wo; }
 };
 
 // 16-B epilogue accesses for the halo convs (p.cperm).  The weight rows are DMA'd into LDS in a
@@ -226,12 +229,22 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
   // wave waits for memory once instead of once per fragment.
   const int rbg = p.rowbias ? rows.group(RM, p.rpg) : 0;
   if (!p.geglu && !p.c_f32 && p.vec && rows.full(RM) && nw + RN * 16 <= p.N && rbg >= 0) {
-    f32x4 badd[RN];
+    // bias and row-bias vectors loaded under one uniform branch each and combined only after the
+    // residual loads are issued: a use inside the branch made hipcc wait (vmcnt(0)) once per column
+    // fragment, four serialised round trips per tile with a row bias (the UNet resnets' time
+    // embedding).  Same adds in the same order: bitwise the previous epilogue.
+    f32x4 bb[RN], rbv[RN];
+    if (p.bias) {
 #pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int n = col_base(perm, nw, j, fq);
-      badd[j] = p.bias ? *(const f32x4*)(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
-      if (p.rowbias) badd[j] += *(const f32x4*)(p.rowbias + (long)rbg * p.rb_ld + n);
+      for (int j = 0; j < RN; ++j) bb[j] = *(const f32x4*)(p.bias + col_base(perm, nw, j, fq));
+    } else {
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (p.rowbias) {
+      const float* rbp = p.rowbias + (long)rbg * p.rb_ld;
+#pragma unroll
+      for (int j = 0; j < RN; ++j) rbv[j] = *(const f32x4*)(rbp + col_base(perm, nw, j, fq));
     }
     f16x4 rr[RM][RN];
     if (p.R) {
@@ -251,6 +264,9 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
         }
       }
     }
+    f32x4 badd[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) badd[j] = p.rowbias ? bb[j] + rbv[j] : bb[j];
     float gs[RN], gq[RN];
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
@@ -427,15 +443,176 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
 }
 
 
+// x + (float)h and fmaf((float)h, (float)h, x), h the low / high f16 half of w: one v_fma_mix_f32 each
+// (the f16 operand converted exactly, one rounding — bitwise the convert-then-add / -fma pair).
+template <bool HI>
+__device__ __forceinline__ float add_h(float x, unsigned w) {
+  float f;
+  if (HI)
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(f) : "v"(w), "v"(x));
+  else
+    asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(f) : "v"(w), "v"(x));
+  return f;
+}
+template <bool HI>
+__device__ __forceinline__ float sq_h(float x, unsigned w) {
+  float f;
+  if (HI)
+    asm("v_fma_mix_f32 %0, %1, %1, %2 op_sel:[1,1,0] op_sel_hi:[1,1,0]" : "=v"(f) : "v"(w), "v"(x));
+  else
+    asm("v_fma_mix_f32 %0, %1, %1, %2 op_sel_hi:[1,1,0]" : "=v"(f) : "v"(w), "v"(x));
+  return f;
+}
+// row16_sum of two values at once, each level one v_add_f32_dpp (v[perm] + v: the same sum as
+// row16_sum's v + v[perm]); the s_nops are the VALU-write → DPP-read wait states, which hipcc does not
+// pad inside inline asm.
+__device__ __forceinline__ void row16_sum2(float& s, float& q) {
+  asm("s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_add_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0xf"
+      : "+v"(s), "+v"(q));
+}
+
+// Specialised epilogue for the common case (whole f16 tile, one row-bias group, no SiLU / GEGLU):
+// residual and GroupNorm moments are template arguments instead of flags tested per fragment
+// (hipcc if-converted the residual add into an add + select per output and re-converted every
+// output to f16 for the moments), the f16 operands enter the f32 sums through v_fma_mix_f32, the
+// row sums are DPP adds, and the moment address is one per-lane base plus a wave-uniform offset.
+// Same operations in the same order as store_tile_t's fast path: bitwise its outputs and moments.
+// The 128-channel GroupNorm-input convs' epilogue is issue-bound beside the partner workgroup's MFMAs
+// (tools/conv_stamp.hip: moments +10 k, residual +4.5 k cycles per wave before this).
+template <int RM, int RN, bool PERM, bool RES, bool MOM, class Rows>
+__device__ __forceinline__ void store_fast(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
+                                           int fr, int fq, int rbg) {
+  static_assert(!PERM || RN % 2 == 0, "16-B permuted accesses pair column fragments");
+  static_assert(RM % 2 == 0, "GroupNorm moments pair 16-row tiles into 32-row blocks");
+  using u32x2 = __attribute__((ext_vector_type(2))) unsigned;
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+  f32x4 bb[RN], rbv[RN];
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bb[j] = *(const f32x4*)(p.bias + col_base(PERM, nw, j, fq));
+  } else {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) bb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (p.rowbias) {
+    const float* rbp = p.rowbias + (long)rbg * p.rb_ld;
+#pragma unroll
+    for (int j = 0; j < RN; ++j) rbv[j] = *(const f32x4*)(rbp + col_base(PERM, nw, j, fq));
+  }
+  u32x2 rr[RM][RN];
+  if constexpr (RES) {
+    // rows of a whole tile are row(0) + i·rstep(): one 64-bit product per tile, the step uniform
+    const f16* const r0 = p.R + (long)bz * p.sR + (long)rows.row(0) * p.ldr;
+    const long rst = (long)rows.rstep() * p.ldr;
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const f16* rrow = r0 + i * rst;
+      if constexpr (PERM) {
+#pragma unroll
+        for (int j = 0; j < RN; j += 2) {
+          const u32x4 v = __builtin_bit_cast(u32x4, *(const f16x8*)(rrow + col_base(true, nw, j, fq)));
+          rr[i][j] = u32x2{v[0], v[1]};
+          rr[i][j + 1] = u32x2{v[2], v[3]};
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RN; ++j) rr[i][j] = __builtin_bit_cast(u32x2, *(const f16x4*)(rrow + col_base(false, nw, j, fq)));
+      }
+    }
+  }
+  f32x4 badd[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) badd[j] = p.rowbias ? bb[j] + rbv[j] : bb[j];
+  // moments: this lane's channel group n >> 2 of column fragment j = lane part + j part
+  float* const gb = MOM ? p.gnp + (long)((nw >> 2) + (PERM ? 2 * fq : fq)) * p.gn_ld : nullptr;
+  f16* const c0 = (f16*)p.C + (long)bz * p.sC + (long)rows.row(0) * p.ldc;
+  const long cst = (long)rows.rstep() * p.ldc;
+  float gs[RN], gq[RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    f16* const crow = c0 + i * cst;
+    u32x2 ow[RN];
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaf(acc[i][j][r], p.alpha, badd[j][r]);
+      if constexpr (RES) {
+        v[0] = add_h<false>(v[0], rr[i][j][0]);
+        v[1] = add_h<true>(v[1], rr[i][j][0]);
+        v[2] = add_h<false>(v[2], rr[i][j][1]);
+        v[3] = add_h<true>(v[3], rr[i][j][1]);
+      }
+      unsigned w0, w1;
+      asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(w0) : "v"(v[0]), "v"(v[1]));
+      asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(w1) : "v"(v[2]), "v"(v[3]));
+      ow[j] = u32x2{w0, w1};
+      if constexpr (!PERM) {
+        *(u32x2*)(crow + col_base(false, nw, j, fq)) = ow[j];
+      } else if (j & 1) {
+        *(u32x4*)(crow + col_base(true, nw, j - 1, fq)) = u32x4{ow[j - 1][0], ow[j - 1][1], w0, w1};
+      }
+      if constexpr (MOM) {
+        float s = add_h<true>(add_h<false>(0.f, w0), w0);
+        s = add_h<true>(add_h<false>(s, w1), w1);
+        float q = sq_h<true>(sq_h<false>(0.f, w0), w0);
+        q = sq_h<true>(sq_h<false>(q, w1), w1);
+        if (!(i & 1)) {
+          gs[j] = s;
+          gq[j] = q;
+        } else {
+          s += gs[j];
+          q += gq[j];
+          row16_sum2(s, q);
+          if (fr == 0) {
+            const int sl = __builtin_amdgcn_readfirstlane((int)rows.slot(i));
+            const long jo = (long)(PERM ? 8 * (j >> 1) + (j & 1) : 4 * j) * p.gn_ld + 2L * sl;
+            *(__attribute__((ext_vector_type(2))) float*)(gb + jo) = {s, q};
+          }
+        }
+      }
+    }
+  }
+}
+
 // The SiLU epilogue (TimestepEmbedding only) is a wave-uniform choice: dispatched here, outside the
-// per-output code, so that no other GEMM / conv computes (and discards) a SiLU per output.
-template <int RM, int RN, int WTN, class Rows>
+// per-output code, so that no other GEMM / conv computes (and discards) a SiLU per output.  Whole
+// f16 tiles without SiLU / GEGLU take store_fast, specialised on residual and moments; PSITE: the
+// call site's usual 16-B permutation (the halo convs' p.cperm), the form store_fast is built for.
+template <int RM, int RN, int WTN, bool PSITE = false, class Rows>
 __device__ __forceinline__ void store_tile(const GemmP& p, f32x4 (&acc)[RM][RN], const Rows& rows, int nw, int bz,
                                            int fr, int fq, bool perm = false) {
-  if (p.silu)
+  if (p.silu) {
     store_tile_t<RM, RN, WTN, true>(p, acc, rows, nw, bz, fr, fq, perm);
-  else
-    store_tile_t<RM, RN, WTN, false>(p, acc, rows, nw, bz, fr, fq, perm);
+    return;
+  }
+  constexpr bool FP = PSITE && RN % 2 == 0;
+  const int rbg = p.rowbias ? rows.group(RM, p.rpg) : 0;
+  if (!p.geglu && !p.c_f32 && p.vec && rows.full(RM) && nw + RN * 16 <= p.N && rbg >= 0 && perm == FP) {
+    if (p.R) {
+      if (p.gnp)
+        store_fast<RM, RN, FP, true, true>(p, acc, rows, nw, bz, fr, fq, rbg);
+      else
+        store_fast<RM, RN, FP, true, false>(p, acc, rows, nw, bz, fr, fq, rbg);
+    } else if (p.gnp) {
+      store_fast<RM, RN, FP, false, true>(p, acc, rows, nw, bz, fr, fq, rbg);
+    } else {
+      store_fast<RM, RN, FP, false, false>(p, acc, rows, nw, bz, fr, fq, rbg);
+    }
+    return;
+  }
+  store_tile_t<RM, RN, WTN, false>(p, acc, rows, nw, bz, fr, fq, perm);
 }
 
 using rdmi::tile_mn;
@@ -1210,10 +1387,10 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   seg(5);
 
   if constexpr (MODE == 3)
-    store_tile<RM, RN, 64>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr, fq,
+    store_tile<RM, RN, 64, true>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr, fq,
                            p.cperm);
   else
-    store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+    store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
   if constexpr (STAMP) {
     wait_vmcnt<0>();
     seg(6);
@@ -1478,7 +1655,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     }
   }
   seg(2);
-  store_tile<RM, RN, 64>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+  store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
   if constexpr (STAMP) {
     wait_vmcnt<0>();
     seg(4);

@@ -17,7 +17,8 @@ from kbench import conv_cases  # noqa: E402
 
 
 def fp(t: torch.Tensor) -> str:
-    v = t.contiguous().view(torch.int16).flatten().to(torch.int64)
+    t = t.contiguous()
+    v = (t.view(torch.int16) if t.element_size() == 2 else t.view(torch.int32)).flatten().to(torch.int64)
     w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 65521 + 1
     return f"{int(v.sum())} {int((v * w).sum() % (1 << 61))}"
 
@@ -39,6 +40,18 @@ def main():
             o2 = K.conv2d(x, w, co, 3, upsample=up, in_gn=(mr, gm, bt, 32, True), residual=res, gn=True)
             o2 = o2[0] if isinstance(o2, tuple) else o2
             print(f"gnconv {lab:32s} {fp(o2)}")
+            print(f"gnmom  {lab:32s} {fp(getattr(o2, K._GN_ATTR))}")
+        # epilogue operand combinations: bias, per-image row bias (the resnets' time embedding),
+        # residual, output moments
+        bias = torch.randn(co, device="cuda", generator=g) * 0.1
+        rowb = torch.randn(B, co, device="cuda", generator=g) * 0.1
+        res = torch.randn(B, Ho, Wo, co, device="cuda", generator=g).half()
+        for tag, kw in (("b", dict(bias=bias)), ("br", dict(bias=bias, rowbias=rowb)),
+                        ("brRm", dict(bias=bias, rowbias=rowb, residual=res, gn=True)),
+                        ("bm", dict(bias=bias, gn=True))):
+            o3 = K.conv2d(x, w, co, 3, upsample=up, **kw)
+            mom = getattr(o3, K._GN_ATTR, None)
+            print(f"ep{tag:5s} {lab:32s} {fp(o3)}" + (f" {fp(mom)}" if mom is not None else ""))
     # implicit-GEMM (non-halo) conv modes: nearest-x2 upsample at 12 -> 24 (Ho % 16 != 0), stride 2
     for lab, B, H, ci, co, kw in [("up 1280 12->24", 4, 12, 1280, 1280, dict(upsample=True)),
                                   ("s2 320 96->48", 4, 96, 320, 320, dict(stride=2)),
@@ -51,6 +64,11 @@ def main():
         a = torch.randn(M, Kd, device="cuda", generator=g).half()
         wl = (torch.randn(N, Kd, device="cuda", generator=g) / math.sqrt(Kd)).half()
         print(f"gemm   M={M} N={N} K={Kd}{'':12s} {fp(K.gemm(a, wl, Kd))}")
+        bias = torch.randn(N, device="cuda", generator=g) * 0.1
+        res = torch.randn(M, N, device="cuda", generator=g).half()
+        og = K.gemm(a, wl, Kd, bias=bias, residual=res, gn=True)
+        mom = getattr(og, K._GN_ATTR, None)
+        print(f"gemmep M={M} N={N} K={Kd}{'':12s} {fp(og)}" + (f" {fp(mom)}" if mom is not None else ""))
     # flash attention (attn_fwd_d64): a fused-QKV layout at the L0 / L1 shapes and ragged key counts
     for B, S, H in [(2, 27648, 5), (2, 6912, 10), (1, 1000, 5), (1, 31, 2)]:
         qkv = torch.randn(B, S, 3 * H * 64, device="cuda", generator=g).half()

@@ -4,7 +4,7 @@
 // 128-channel shape: 768² 128 → 128, B images, GroupNorm+SiLU input, residual and GroupNorm moments
 // out (the VAE ResnetBlock2D conv2).  Read the SHARES, not the stamped build's run time.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/conv_stamp.hip -o tools/conv_stamp
-//   ./tools/conv_stamp [B] [HW] [gn res moments: 0/1 each] [Cin] [Cout]
+//   ./tools/conv_stamp [B] [HW] [gn res moments: 0/1 each] [Cin] [Cout] [residual row stride]
 // Cout = 128: conv_halo_occ2_kernel; Cout % 256 == 0: conv_halo_kernel<1, 2, 4, GN> (8 waves, ping-pong).
 #include "../rollingdepth_amd/csrc/gemm_kernels.h"
 
@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
   const bool gn = argc > 3 ? atoi(argv[3]) : 1, res = argc > 4 ? atoi(argv[4]) : 1, mom = argc > 5 ? atoi(argv[5]) : 1;
   const int Cin = argc > 6 ? atoi(argv[6]) : 128, Cout = argc > 7 ? atoi(argv[7]) : 128, Kp = 9 * Cin, G = 32;
   const bool wide = Cout % 256 == 0;
+  const int rld = argc > 8 ? atoi(argv[8]) : Cout;  // residual row stride (0: every row reads one cached row)
   const int WPG = wide ? 8 : 4;  // waves per workgroup
   const long M = (long)B * HW * HW;
   f16 *x, *w, *y, *r;
@@ -71,7 +72,7 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_f, dim3(1), dim3(256), 0, 0, bet, (long)Cin, 0.05f, -0.05f);
   GemmP p{};
   p.A = x; p.Wt = w; p.ldw = Kp; p.C = y; p.ldc = Cout; p.alpha = 1.f;
-  p.R = res ? r : nullptr; p.ldr = Cout; p.rpg = HW * HW;
+  p.R = res ? r : nullptr; p.ldr = rld; p.rpg = HW * HW;
   p.M = (int)M; p.N = Cout; p.K = Kp; p.Kvalid = Kp;
   p.IH = HW; p.IW = HW; p.Cin = Cin; p.Ho = HW; p.Wo = HW; p.kh = 3; p.kw = 3; p.stride = 1; p.pt = 1; p.pl = 1;
   p.cin_vecs = Cin / 8; p.cmaj = 1; p.vec = 1;
