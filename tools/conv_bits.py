@@ -69,6 +69,12 @@ def main():
         og = K.gemm(a, wl, Kd, bias=bias, residual=res, gn=True)
         mom = getattr(og, K._GN_ATTR, None)
         print(f"gemmep M={M} N={N} K={Kd}{'':12s} {fp(og)}" + (f" {fp(mom)}" if mom is not None else ""))
+    # GroupNorm(+SiLU) apply pass at the UNet / VAE shapes that run it unfused
+    for B, H, C in [(6, 96, 320), (6, 48, 640), (6, 24, 1280), (5, 12, 2560), (3, 96, 512)]:
+        x = torch.randn(B, H, H, C, device="cuda", generator=g).half()
+        gm, bt = torch.rand(C, device="cuda", generator=g) + 0.5, torch.randn(C, device="cuda", generator=g) * 0.1
+        for silu in (True, False):
+            print(f"gnapp  B={B} {H}^2 C={C} silu={int(silu)}{'':10s} {fp(K.groupnorm(x, gm, bt, 32, 1e-5, silu))}")
     # flash attention (attn_fwd_d64): a fused-QKV layout at the L0 / L1 shapes and ragged key counts
     for B, S, H in [(2, 27648, 5), (2, 6912, 10), (1, 1000, 5), (1, 31, 2)]:
         qkv = torch.randn(B, S, 3 * H * 64, device="cuda", generator=g).half()
