@@ -128,6 +128,11 @@ def bench_gemm(iters):
                                  ("L0 proj 221k x 320 x 320 +res", 221184, 320, 320, False),
                                  ("L0 proj 691k x 320 x 320 +res (x75)", 691200, 320, 320, False),
                                  ("L0 qkv 691k x 960 x 320 (x75)", 691200, 960, 320, False),
+                                 ("L0 ff1 geglu 691k x 2560 x 320 (x75)", 691200, 2560, 320, True),
+                                 ("L0 ff2 691k x 320 x 1280 +res (x75)", 691200, 320, 1280, False),
+                                 ("L1 proj 173k x 640 x 640 +res (x75)", 172800, 640, 640, False),
+                                 ("L1 ff1 geglu 173k x 5120 x 640 (x75)", 172800, 5120, 640, True),
+                                 ("L2 proj 43k x 1280 x 1280 +res (x75)", 43200, 1280, 1280, False),
                                  ("L1 proj 55k x 640 x 640 +res", 55296, 640, 640, False),
                                  ("L1 ff1 geglu 55k x 5120 x 640", 55296, 5120, 640, True),
                                  ("L0 ff2 221k x 320 x 1280", 221184, 320, 1280, False),
