@@ -551,6 +551,11 @@ class RollingDepthPipeline:
                                              record, generator)
         # ----------------- encode (H2D boundary :263)
         frames = input_frames[0].to(self.device)
+        # input_rgb = frames / 2 + 0.5 in f16 as the reference computes it on the host (x/2 is exact,
+        # the +0.5 rounds identically), evaluated on the device; its D2H copy is queued now so that it
+        # runs under the denoising instead of at the end of the call
+        d2h = torch.cuda.Stream(self.device)
+        rgb_host = self._to_host_async(frames.to(self.dtype) / 2.0 + 0.5, d2h)
         rgb_latent = self.encode_rgb(frames)
         N, h, w, _ = rgb_latent.shape
         # ----------------- shared init noise (:282-288)
@@ -561,7 +566,6 @@ class RollingDepthPipeline:
                                            record=record)
         # snippet_ls D2H (the reference returns it on the host) overlaps the aligner's kernels
         H, W = snippets[0].shape[-2:]
-        d2h = torch.cuda.Stream(self.device)
         snip_host = [self._to_host_async(s.to(self.dtype).view(s.shape[0], s.shape[1], 1, H, W), d2h)
                      for s in snippets]
         # ----------------- co-alignment + renormalisation (:306-318)
@@ -588,10 +592,7 @@ class RollingDepthPipeline:
         else:
             depth = coaligned
         # ----------------- outputs (:345-353, D2H boundary; pinned, async, one sync)
-        # input_rgb = frames / 2 + 0.5 in f16 as the reference computes it on the host (x/2 is exact,
-        # the +0.5 rounds identically), evaluated on the device before the copy
-        rgb = input_frames[0].to(self.device, self.dtype) / 2.0 + 0.5
-        outs = [self._to_host_async(t, d2h) for t in (rgb, depth, coaligned)]
+        outs = [self._to_host_async(t, d2h) for t in (depth, coaligned)]
         d2h.synchronize()
-        return RollingDepthOutput(input_rgb=outs[0], depth_pred=outs[1], snippet_ls=snip_host,
-                                  depth_coaligned=outs[2])
+        return RollingDepthOutput(input_rgb=rgb_host, depth_pred=outs[0], snippet_ls=snip_host,
+                                  depth_coaligned=outs[1])
