@@ -1571,6 +1571,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   asm volatile("" ::: "memory");
 
   const int wms = __builtin_amdgcn_readfirstlane(wm);
+  const bool live = n0 + (wids & 1) * 64 < p.N;  // wave-uniform
   seg(0);
   for (int u = 0; u < nk; ++u) {
     const int cb = u / 9;
@@ -1608,54 +1609,60 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
       const unsigned a = kh ? (aoff[i & 3] ^ 64u) : aoff[i & 3];
       return *(const f16x8*)((const char*)lds + a + i * HWD * BKP * 2);
     };
-    if constexpr (PIPE) {
-      // Software-pipelined fragment reads over the K-tile's 16 MFMA groups s = (kh, i): A(s+2) is
-      // read while group s's 4 MFMAs issue, the second k half's B fragments 3 groups ahead of their
-      // first use (≈44 live fragment registers instead of 96: with the f32 accumulators the
-      // all-reads-first form ran out of registers, and the compiler then serialised every A read
-      // behind lgkmcnt(0) in front of its MFMAs).  The sched_group_barrier sequence pins the issue
-      // order (the scheduler otherwise sinks each read to just before its use).
-      constexpr int NS = 2 * RM, PD = 2, BPRE = RM - 3;
-      f16x8 bfr[2][RN], ar[PD + 1];
+    // a wave whose 64 columns all lie past N (the ragged last 128-channel tile of a Cout = 320 conv)
+    // issues no fragment reads or MFMAs: its SIMD's matrix pipe goes to the co-resident workgroup
+    if (live) {
+      if constexpr (PIPE) {
+        // Software-pipelined fragment reads over the K-tile's 16 MFMA groups s = (kh, i): A(s+2) is
+        // read while group s's 4 MFMAs issue, the second k half's B fragments 3 groups ahead of their
+        // first use (≈44 live fragment registers instead of 96: with the f32 accumulators the
+        // all-reads-first form ran out of registers, and the compiler then serialised every A read
+        // behind lgkmcnt(0) in front of its MFMAs).  The sched_group_barrier sequence pins the issue
+        // order (the scheduler otherwise sinks each read to just before its use).
+        constexpr int NS = 2 * RM, PD = 2, BPRE = RM - 3;
+        f16x8 bfr[2][RN], ar[PD + 1];
 #pragma unroll
-      for (int j = 0; j < RN; ++j) bfr[0][j] = *(const f16x8*)(lb + j * 16 * BKP + off0);
+        for (int j = 0; j < RN; ++j) bfr[0][j] = *(const f16x8*)(lb + j * 16 * BKP + off0);
 #pragma unroll
-      for (int q = 0; q < PD; ++q) ar[q] = readA(q / RM, q % RM);
+        for (int q = 0; q < PD; ++q) ar[q] = readA(q / RM, q % RM);
 #pragma unroll
-      for (int st = 0; st < NS; ++st) {
-        if (st == BPRE) {
+        for (int st = 0; st < NS; ++st) {
+          if (st == BPRE) {
 #pragma unroll
-          for (int j = 0; j < RN; ++j) bfr[1][j] = *(const f16x8*)(lb + j * 16 * BKP + off1);
-        }
-        if (st + PD < NS) ar[(st + PD) % (PD + 1)] = readA((st + PD) / RM, (st + PD) % RM);
-        const int kh = st / RM, i = st % RM;
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[kh][j], ar[st % (PD + 1)], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, RN + PD, 0);
-      occ2_sched<RN, PD, NS, BPRE>(std::make_integer_sequence<int, NS>{});
-    } else {
-      f16x8 af[2][RM], bf[2][RN];
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh) {
-        const int off = kh ? off1 : off0;
-#pragma unroll
-        for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
-#pragma unroll
-        for (int i = 0; i < RM; ++i) af[kh][i] = readA(kh, i);
-      }
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-        for (int i = 0; i < RM; ++i)
+            for (int j = 0; j < RN; ++j) bfr[1][j] = *(const f16x8*)(lb + j * 16 * BKP + off1);
+          }
+          if (st + PD < NS) ar[(st + PD) % (PD + 1)] = readA((st + PD) / RM, (st + PD) % RM);
+          const int kh = st / RM, i = st % RM;
 #pragma unroll
           for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[kh][j], ar[st % (PD + 1)], acc[i][j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, RN + PD, 0);
+        occ2_sched<RN, PD, NS, BPRE>(std::make_integer_sequence<int, NS>{});
+      } else {
+        f16x8 af[2][RM], bf[2][RN];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const int off = kh ? off1 : off0;
+#pragma unroll
+          for (int j = 0; j < RN; ++j) bf[kh][j] = *(const f16x8*)(lb + j * 16 * BKP + off);
+#pragma unroll
+          for (int i = 0; i < RM; ++i) af[kh][i] = readA(kh, i);
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
+      }
     }
   }
   seg(2);
-  store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+  if (live)
+    store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq,
+                                 p.cperm);
   if constexpr (STAMP) {
     wait_vmcnt<0>();
     seg(4);
@@ -2058,6 +2065,7 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
   const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
   const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
 
+  const bool live = n0 + (wids & 1) * 64 < p.N;  // wave-uniform
   issue(0);
   wait_vmcnt<0>();
   asm volatile("" ::: "memory");
@@ -2071,6 +2079,7 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
       asm volatile("" ::: "memory");
     }
     if (u + 1 < nk) issue(u + 1);
+    if (!live) continue;  // columns all past N (the ragged last tile of N = 320 / 960): no reads, no MFMAs
     const f16* la = lds + (u & 1) * SLOT + (wm * 64) * BKP;
     const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * 64) * BKP;
     f16x8 af[2][RM], bf[2][RN];
@@ -2090,7 +2099,7 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
   }
-  store_tile<RM, RN, 64>(p, acc, LinRows{m0 + wm * 64, fr, p.M}, n0 + wn * 64, bz, fr, fq);
+  if (live) store_tile<RM, RN, 64>(p, acc, LinRows{m0 + wm * 64, fr, p.M}, n0 + wn * 64, bz, fr, fq);
 }
 
 // Launchers, one translation unit per engine family (gemm_classic.hip, gemm_pp.hip, conv_halo.hip,
