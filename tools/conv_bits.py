@@ -80,6 +80,13 @@ def main():
         qkv = torch.randn(B, S, 3 * H * 64, device="cuda", generator=g).half()
         q, k, v = qkv[..., :H * 64], qkv[..., H * 64:2 * H * 64], qkv[..., 2 * H * 64:]
         print(f"attn   B={B} S={S} H={H}{'':18s} {fp(K.attention(q, k, v, H))}")
+    # VAE mid-block attention at d = 512 (attn_fwd_d512): pipeline shape, ragged keys, growing scores
+    for B, S, Sk, grow in [(2, 9216, 9216, False), (1, 300, 77, False), (1, 640, 640, True)]:
+        q = torch.randn(B, S, 512, device="cuda", generator=g).half()
+        gk = torch.linspace(0.2, 4.0, Sk, device="cuda")[None, :, None] if grow else 1.0
+        k = (torch.randn(B, Sk, 512, device="cuda", generator=g) * gk).half()
+        v = torch.randn(B, Sk, 512, device="cuda", generator=g).half()
+        print(f"attn512 B={B} S={S} Sk={Sk} grow={int(grow)}{'':8s} {fp(K.attention_d512(q, k, v, 512 ** -0.5))}")
     torch.cuda.synchronize()
 
 
