@@ -60,7 +60,8 @@ def main():
         w = K.pack_conv(torch.randn(co, ci, 3, 3, generator=torch.Generator().manual_seed(2)) / math.sqrt(ci * 9),
                         "cuda", ci)
         print(f"conv   {lab:32s} {fp(K.conv2d(x, w, co, 3, **kw))}")
-    for M, N, Kd in [(4096, 320, 320), (4096, 2560, 320), (2048, 1280, 1280), (4096, 960, 320), (1024, 10240, 1280)]:
+    for M, N, Kd in [(4096, 320, 320), (4096, 2560, 320), (2048, 1280, 1280), (4096, 960, 320), (1024, 10240, 1280),
+                     (3000, 5120, 640)]:
         a = torch.randn(M, Kd, device="cuda", generator=g).half()
         wl = (torch.randn(N, Kd, device="cuda", generator=g) / math.sqrt(Kd)).half()
         print(f"gemm   M={M} N={N} K={Kd}{'':12s} {fp(K.gemm(a, wl, Kd))}")
@@ -69,6 +70,8 @@ def main():
         og = K.gemm(a, wl, Kd, bias=bias, residual=res, gn=True)
         mom = getattr(og, K._GN_ATTR, None)
         print(f"gemmep M={M} N={N} K={Kd}{'':12s} {fp(og)}" + (f" {fp(mom)}" if mom is not None else ""))
+        if N % 128 == 0:  # GEGLU epilogue (value / gate halves interleaved per 64-column slab)
+            print(f"geglu  M={M} N={N} K={Kd}{'':12s} {fp(K.gemm(a, wl, Kd, bias=bias, geglu=True))}")
     # GroupNorm(+SiLU) apply pass at the UNet / VAE shapes that run it unfused
     for B, H, C in [(6, 96, 320), (6, 48, 640), (6, 24, 1280), (5, 12, 2560), (3, 96, 512)]:
         x = torch.randn(B, H, H, C, device="cuda", generator=g).half()
