@@ -427,7 +427,11 @@ __device__ __forceinline__ void store_tile_t(const GemmP& p, f32x4 (&acc)[RM][RN
           const float h = acc[i][j][r] * p.alpha + bh[j][r];
           const float g = acc[i][j + RN / 2][r] * p.alpha + bg[j][r];
           v[r] = h * gelu_erf_fast(g);  // no per-element flag: hipcc would branch on it per output
-          if (p.R) v[r] += (float)p.R[rbz + (long)m * p.ldr + no + r];
+        }
+        if (p.R) {  // one wave-uniform branch per 4 outputs (inside the loop hipcc branched per output)
+          const f16* rp = p.R + rbz + (long)m * p.ldr + no;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)rp[r];
         }
         if (p.c_f32) {
           *(f32x4*)((float*)p.C + crow + no) = f32x4{v[0], v[1], v[2], v[3]};
