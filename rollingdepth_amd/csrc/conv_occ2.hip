@@ -30,8 +30,11 @@ void launch_conv_h32(bool gn, dim3 g, hipStream_t s, const GemmP& p) {
     hipLaunchKernelGGL((conv_halo32_kernel<false>), g, dim3(256), 0, s, p);
 }
 
-void launch_gemm_occ2(dim3 g, hipStream_t s, const GemmP& p) {
-  hipLaunchKernelGGL((gemm_occ2_kernel<0>), g, dim3(256), 0, s, p);
+void launch_gemm_occ2(int bn, dim3 g, hipStream_t s, const GemmP& p) {
+  if (bn == 160)
+    hipLaunchKernelGGL((gemm_occ2_kernel<0, 160>), g, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_occ2_kernel<0, 128>), g, dim3(256), 0, s, p);
 }
 
 }  // namespace rdmi_gk

@@ -131,6 +131,152 @@ __global__ __launch_bounds__(HT) void head_taps_v(const T* __restrict__ x, long 
   }
 }
 
+// pass 1 at LPP = 16 (C = 128: the SD VAE decoder's head, the one the pipeline runs): head_taps_v's
+// arithmetic, operation for operation (bitwise its taps), issued leaner — hipcc's form of it was
+// vector-issue-bound at ≈230 instructions per pixel group:
+//  * tap pairs (0,1) (2,3) (4,5) (6,7) as packed FMAs: v_pk_fma_f32 takes the channel's value from
+//    one half of a register pair (op_sel) and does the two taps' FMAs, each rounding as v_fma_f32;
+//  * the butterfly's DPP moves fused into the adds (v_add_f32_dpp: 36 instructions, not 72);
+//  * the tap a lane writes picked by lane masks computed once (hipcc built a 9-way branch tree);
+//  * the next pixel's 16 bytes loaded before this pixel's arithmetic.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int LO>  // acc.xy += y[LO] * w.xy
+__device__ __forceinline__ void pk_fma_lo(f32x2& acc, f32x2 y, f32x2 w) {
+  if constexpr (LO == 0)
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(y), "v"(w));
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(y), "v"(w));
+}
+
+// Σ over the 16 lanes of a row, xor-butterfly order (group_sum<16>), for nine values at once: nine
+// independent adds per level, so one s_nop covers the DPP read-after-VALU-write hazard at entry.
+__device__ __forceinline__ void group16_sum9(float& a0, float& a1, float& a2, float& a3, float& a4, float& a5,
+                                             float& a6, float& a7, float& a8) {
+#define RDMI_L9(CTL)                                                       \
+  "v_add_f32_dpp %0, %0, %0 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %1, %1, %1 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %2, %2, %2 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %3, %3, %3 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %4, %4, %4 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %5, %5, %5 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %6, %6, %6 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %7, %7, %7 " CTL " row_mask:0xf bank_mask:0xf\n\t"        \
+  "v_add_f32_dpp %8, %8, %8 " CTL " row_mask:0xf bank_mask:0xf\n\t"
+  asm("s_nop 1\n\t" RDMI_L9("quad_perm:[1,0,3,2]") RDMI_L9("quad_perm:[2,3,0,1]") RDMI_L9("row_half_mirror")
+          RDMI_L9("row_mirror")
+      : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8));
+#undef RDMI_L9
+}
+
+// 16 input bytes / 32 (f32) of one lane, loaded raw: the conversion waits for the load, so the
+// prefetch of the next pixel holds the raw registers, not converted values.
+template <typename T>
+struct Raw8;
+template <>
+struct Raw8<f16> {
+  f16x8 r;
+  __device__ __forceinline__ void load(const f16* p) { r = *(const f16x8*)p; }
+  __device__ __forceinline__ float operator[](int e) const { return (float)r[e]; }
+};
+template <>
+struct Raw8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *(const f32x4*)p;
+    b = *(const f32x4*)(p + 4);
+  }
+  __device__ __forceinline__ float operator[](int e) const { return e < 4 ? a[e] : b[e - 4]; }
+};
+
+template <typename T, bool SILU>
+struct Head16 {
+  float sc[8], sh[8];
+  f32x2 wp[4][8];  // taps (2i, 2i+1) of channel c0 + e
+  float w8[8];     // tap 8
+  int cl;
+
+  __device__ __forceinline__ void pixel(const Raw8<T>& v, float* __restrict__ dq) const {
+    f32x2 y[4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float f = fmaf(v[e], sc[e], sh[e]);
+      if constexpr (SILU) f = sizeof(T) == 2 ? silu_f(f) : f / (1.0f + expf(-f));
+      y[e >> 1][e & 1] = f;
+    }
+    f32x2 a[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = f32x2{0.f, 0.f};  // first step fma(y, w, 0) as head_taps_v's
+    float a8 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (e & 1)
+          pk_fma_lo<1>(a[i], y[e >> 1], wp[i][e]);
+        else
+          pk_fma_lo<0>(a[i], y[e >> 1], wp[i][e]);
+      }
+      a8 = fmaf(y[e >> 1][e & 1], w8[e], a8);
+    }
+    float s0 = a[0].x, s1 = a[0].y, s2 = a[1].x, s3 = a[1].y, s4 = a[2].x, s5 = a[2].y, s6 = a[3].x, s7 = a[3].y;
+    group16_sum9(s0, s1, s2, s3, s4, s5, s6, s7, a8);
+    float o = s0;
+    o = cl == 1 ? s1 : o;
+    o = cl == 2 ? s2 : o;
+    o = cl == 3 ? s3 : o;
+    o = cl == 4 ? s4 : o;
+    o = cl == 5 ? s5 : o;
+    o = cl == 6 ? s6 : o;
+    o = cl == 7 ? s7 : o;
+    o = cl == 8 ? a8 : o;
+    if (cl < 9) dq[cl] = o;  // tap cl written by lane cl of the group
+  }
+};
+
+template <typename T, bool SILU>
+__global__ __launch_bounds__(HT) void head_taps_16(const T* __restrict__ x, long HW, int G,
+                                                   const float* __restrict__ mr, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, const float* __restrict__ w,
+                                                   float* __restrict__ d, long P, int ppb) {
+  constexpr int C = 128, LPP = 16, S = HT / LPP;
+  const int b = blockIdx.y;
+  Head16<T, SILU> h;
+  h.cl = threadIdx.x % LPP;
+  const int c0 = h.cl * 8;
+  const int cpg = C / G;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e, g = c / cpg;
+    const float mean = mr[2 * (b * G + g)], rstd = mr[2 * (b * G + g) + 1];
+    h.sc[e] = rstd * gamma[c];
+    h.sh[e] = beta[c] - mean * h.sc[e];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h.wp[i][e] = f32x2{w[(2 * i) * C + c], w[(2 * i + 1) * C + c]};
+    h.w8[e] = w[8 * C + c];
+  }
+  const long pbeg = (long)blockIdx.x * ppb;
+  const long pend = pbeg + ppb < HW ? pbeg + ppb : HW;
+  long p = pbeg + threadIdx.x / LPP;
+  if (p >= pend) return;
+  const T* xb = x + (long)b * HW * C + c0;
+  float* db = d + (long)b * HW * 9;
+  // two raw buffers in turn; the next pixel's load is unconditional (clamped to the last pixel) so
+  // that the wait before each pixel's arithmetic counts only the older load
+  Raw8<T> ra, rb;
+  ra.load(xb + p * C);
+  for (;;) {
+    rb.load(xb + (p + S < pend ? p + S : pend - 1) * C);
+    h.pixel(ra, db + p * 9);
+    p += S;
+    if (p >= pend) break;
+    ra.load(xb + (p + S < pend ? p + S : pend - 1) * C);
+    h.pixel(rb, db + p * 9);
+    p += S;
+    if (p >= pend) break;
+  }
+}
+
 // pass 2 for the pixel-major taps: out[q] = bias + Σ_{dy,dx} d[q + (dy-1)·W + dx-1][3dy+dx]
 template <typename T>
 __global__ __launch_bounds__(HT) void head_gather_v(const float* __restrict__ d, int H, int W, long P, float bias,
@@ -199,7 +345,15 @@ int head_launch(const void* x, int B, int H, int W, int C, int G, const float* m
                          beta, w, workspace, P, PPB);                                                            \
     break;
     switch (lpp) {
-      RDMI_HEAD(1) RDMI_HEAD(2) RDMI_HEAD(4) RDMI_HEAD(8) RDMI_HEAD(16) RDMI_HEAD(32) RDMI_HEAD(64)
+      case 16:
+        if (silu)
+          hipLaunchKernelGGL((head_taps_16<T, true>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma, beta,
+                             w, workspace, P, PPB);
+        else
+          hipLaunchKernelGGL((head_taps_16<T, false>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma, beta,
+                             w, workspace, P, PPB);
+        break;
+      RDMI_HEAD(1) RDMI_HEAD(2) RDMI_HEAD(4) RDMI_HEAD(8) RDMI_HEAD(32) RDMI_HEAD(64)
       default: break;
     }
 #undef RDMI_HEAD

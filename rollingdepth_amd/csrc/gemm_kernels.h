@@ -2012,11 +2012,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
 // wait for the own DMA of this K-tile (issued one K-tile earlier) and the own fragment reads of
 // the previous one, one barrier, issue the next K-tile into the other slot, 16 fragment reads,
 // 32 MFMAs.  LDS rows are 128 B with 16-B chunk c of row r at c ^ (r & 7) (as gemm_pp_kernel).
-template <int V = 0>
+// BN = 160 (N % 160 == 0: the L0 N = 320 / 960 Linears): 64×80 per wave, a 72-KiB ring — two column
+// tiles of N = 320 instead of two and a half-dead third, so A is read twice, not three times, and no
+// workgroup slot holds dead waves.  Same MFMA operands and order per output: bitwise the BN = 128 tile.
+template <int V = 0, int BN = 128>
 __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
-  constexpr int BM = 128, BN = 128, BKP = 64, RM = 4, RN = 4;
-  constexpr int NA = 4, NB = 4;            // 1-KiB DMA pieces per wave per K-tile (16 / 4 waves each)
-  constexpr int SLOT = (BM + BN) * BKP;    // halves (32 KiB)
+  constexpr int BM = 128, BKP = 64, RM = 4, RN = BN / 32, WN = BN / 2;
+  constexpr int NA = 4, NB = BN / 32;      // 1-KiB DMA pieces per wave per K-tile (BM / 8 and BN / 8 over 4 waves)
+  constexpr int SLOT = (BM + BN) * BKP;    // halves (32 / 36 KiB)
   __shared__ __attribute__((aligned(16))) f16 lds[2 * SLOT];
 
   const int tid = threadIdx.x;
@@ -2069,7 +2072,7 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
   const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
   const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
 
-  const bool live = n0 + (wids & 1) * 64 < p.N;  // wave-uniform
+  const bool live = n0 + (wids & 1) * WN < p.N;  // wave-uniform
   issue(0);
   wait_vmcnt<0>();
   asm volatile("" ::: "memory");
@@ -2085,7 +2088,7 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
     if (u + 1 < nk) issue(u + 1);
     if (!live) continue;  // columns all past N (the ragged last tile of N = 320 / 960): no reads, no MFMAs
     const f16* la = lds + (u & 1) * SLOT + (wm * 64) * BKP;
-    const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * 64) * BKP;
+    const f16* lb = lds + (u & 1) * SLOT + BM * BKP + (wn * WN) * BKP;
     f16x8 af[2][RM], bf[2][RN];
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
@@ -2103,14 +2106,14 @@ __global__ __launch_bounds__(256, 2) void gemm_occ2_kernel(GemmP p) {
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[kh][j], af[kh][i], acc[i][j], 0, 0, 0);
   }
-  if (live) store_tile<RM, RN, 64>(p, acc, LinRows{m0 + wm * 64, fr, p.M}, n0 + wn * 64, bz, fr, fq);
+  if (live) store_tile<RM, RN, WN>(p, acc, LinRows{m0 + wm * 64, fr, p.M}, n0 + wn * WN, bz, fr, fq);
 }
 
 // Launchers, one translation unit per engine family (gemm_classic.hip, gemm_pp.hip, conv_halo.hip,
 // conv_occ2.hip) so that the engines compile in parallel; the dispatch (gemm.hip) calls these.
 void launch_gemm_classic(int mode, int bm, int bn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_gemm_pp(int mode, int wm, int dbg, dim3 g, hipStream_t s, const GemmP& p);
-void launch_gemm_occ2(dim3 g, hipStream_t s, const GemmP& p);
+void launch_gemm_occ2(int bn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_halo(int mode, int nph, int wn, bool gn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_occ2(int mode, bool gn, bool pipe, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_h32(bool gn, dim3 g, hipStream_t s, const GemmP& p);

@@ -78,6 +78,16 @@ def main():
         gm, bt = torch.rand(C, device="cuda", generator=g) + 0.5, torch.randn(C, device="cuda", generator=g) * 0.1
         for silu in (True, False):
             print(f"gnapp  B={B} {H}^2 C={C} silu={int(silu)}{'':10s} {fp(K.groupnorm(x, gm, bt, 32, 1e-5, silu))}")
+    # decoder head (GroupNorm+SiLU -> 3x3 conv to one channel): f16 / f32 input, f16 / f32 output,
+    # a ragged pixel count per workgroup (HW % 1024 != 0)
+    for B, H, W, xdt, odt in [(3, 768, 768, torch.float16, torch.float32), (2, 96, 100, torch.float16, torch.float16),
+                              (2, 64, 72, torch.float32, torch.float32)]:
+        x = (torch.randn(B, H, W, 128, device="cuda", generator=g) * 2 + 0.3).to(xdt)
+        gm, bt = torch.rand(128, device="cuda", generator=g) + 0.5, torch.randn(128, device="cuda", generator=g) * 0.1
+        w9 = torch.randn(9, 128, device="cuda", generator=g) / 30
+        for silu in (True, False):
+            y = K.conv3x3_to1_gn(x, gm, bt, 32, 1e-6, silu, w9, 0.1, out_dtype=odt)
+            print(f"head   B={B} {H}x{W} {str(xdt)[6:]}->{str(odt)[6:]} silu={int(silu)}{'':4s} {fp(y)}")
     # flash attention (attn_fwd_d64): a fused-QKV layout at the L0 / L1 shapes and ragged key counts
     for B, S, H in [(2, 27648, 5), (2, 6912, 10), (1, 1000, 5), (1, 31, 2)]:
         qkv = torch.randn(B, S, 3 * H * 64, device="cuda", generator=g).half()
