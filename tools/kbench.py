@@ -58,6 +58,20 @@ def bench_conv(iters):
         print(f"conv  {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s")
 
 
+def bench_conv1(iters):
+    """1×1 convs (ResnetBlock2D shortcuts) at the pipeline's launch shapes: dense GEMMs over pixels."""
+    for lab, B, H, ci, co in [("vae sc 256->128 768^2 x5", 5, 768, 256, 128), ("vae sc 512->256 384^2 x9", 9, 384, 512, 256),
+                              ("unet sc 640->320 96^2 x75", 75, 96, 640, 320), ("unet sc 960->320 96^2 x75", 75, 96, 960, 320),
+                              ("unet sc 1280->640 48^2 x75", 75, 48, 1280, 640)]:
+        x = torch.randn(B, H, H, ci, device="cuda").half()
+        w = K.pack_conv(torch.randn(co, ci, 1, 1) / math.sqrt(ci), "cuda", ci)
+        out = torch.empty(B, H, H, co, device="cuda", dtype=torch.float16)
+        ms = timeit(lambda: K.conv2d(x, w, co, 1, pad=0, out=out), iters)
+        fl = 2.0 * B * H * H * co * ci
+        by = 2.0 * B * H * H * (ci + co)
+        print(f"conv1 {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s {by / ms / 1e6:7.0f} GB/s")
+
+
 def bench_head(iters):
     """Decoder head: GroupNorm+SiLU+3x3 conv to one channel (rdmi_conv3x3_to1_gn)."""
     for B, H, C in [(16, 768, 128), (8, 768, 128)]:
@@ -293,4 +307,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"attn512": bench_attn512, "conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
+        {"attn512": bench_attn512, "conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "conv1": bench_conv1, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
