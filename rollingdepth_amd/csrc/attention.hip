@@ -828,7 +828,20 @@ __global__ __launch_bounds__(256) void softmax_rows_reg_k(const float* __restric
 // row: LN moments (same order as layernorm_k), H dot products against w (LDS), the sigmoid
 // weights, the output row — one read and one write of the row instead of LN + q GEMM + attention
 // + out GEMM (five row passes).  w, u, c are folded once per context (unet.Transformer).
-template <int NV>  // f16x8 vectors per lane: C ≤ 512·NV
+// HC > 0: H = HC at compile time — the H head dot products are formed first and their wave sums
+// run level by level together (H independent shuffle chains in flight instead of H serial ones), then
+// the sigmoids and the output accumulation in head order: the same operations on every value as the
+// HC = 0 loop, bitwise its output (the per-row latency of 2 + H dependent reductions was the bound:
+// ≈1.75 TB/s at C = 320, 0.9 at 640).
+template <int HC>
+__device__ __forceinline__ void wave_sum_n(float (&d)[HC]) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int h = 0; h < HC; ++h) d[h] += __shfl_xor(d[h], o, 64);
+}
+
+template <int NV, int HC = 0>  // f16x8 vectors per lane: C ≤ 512·NV
 __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f16* __restrict__ y, long M, int C,
                                                     int H, const float* __restrict__ g, const float* __restrict__ b,
                                                     float eps, const float* __restrict__ wd,
@@ -897,7 +910,40 @@ __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f
         n[i][e] = lane + 64 * i < CV ? (float)(f16)(((float)v[i][e] - mean) * rstd * gr[i][e] + br[i][e]) : 0.f;
         o[i][e] = 0.f;
       }
-    for (int h = 0; h < H; ++h) {
+    if constexpr (HC > 0) {
+      float d[HC];
+#pragma unroll
+      for (int h = 0; h < HC; ++h) {
+        d[h] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int cv = lane + 64 * i;
+          if (cv < CV) {
+            const f32x4 w0 = *(const f32x4*)(ws + h * C + cv * 8), w1 = *(const f32x4*)(ws + h * C + cv * 8 + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[h] = fmaf(n[i][e], w0[e], fmaf(n[i][4 + e], w1[e], d[h]));
+          }
+        }
+      }
+      wave_sum_n<HC>(d);
+#pragma unroll
+      for (int h = 0; h < HC; ++h) {
+        const float ph = 1.0f / (1.0f + __expf(-d[h]));
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int cv = lane + 64 * i;
+          if (cv < CV) {
+            const f32x4 u0 = *(const f32x4*)(us + h * C + cv * 8), u1 = *(const f32x4*)(us + h * C + cv * 8 + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              o[i][e] = fmaf(ph, u0[e], o[i][e]);
+              o[i][4 + e] = fmaf(ph, u1[e], o[i][4 + e]);
+            }
+          }
+        }
+      }
+    }
+    for (int h = 0; h < (HC > 0 ? 0 : H); ++h) {
       float d = 0.f;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -1016,15 +1062,22 @@ extern "C" int rdmi_cross_attn_pair(const void* x, void* y, long M, int C, int H
   long blocks = (M + 3) / 4;
   if (blocks > 4096) blocks = 4096;
   const int nv = (C / 8 + 63) / 64;
-#define RDMI_PAIR(NVV) \
-  hipLaunchKernelGGL(attn2_pair_k<NVV>, dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, (const f16*)x, \
-                     (f16*)y, M, C, H, ln_gamma, ln_beta, eps, w, u, c)
-  if (nv == 1)
-    RDMI_PAIR(1);
+#define RDMI_PAIR(NVV, HCC) \
+  hipLaunchKernelGGL((attn2_pair_k<NVV, HCC>), dim3((unsigned)blocks), dim3(256), lds, (hipStream_t)stream, \
+                     (const f16*)x, (f16*)y, M, C, H, ln_gamma, ln_beta, eps, w, u, c)
+  // the SD2 UNet's L0 / L1 blocks (5 / 10 heads) with the heads unrolled (RDMI_PAIR_HC=0: the loop, A/B)
+  const char* ehc = getenv("RDMI_PAIR_HC");
+  const bool hc = !(ehc && ehc[0] == '0');
+  if (nv == 1 && H == 5 && hc)
+    RDMI_PAIR(1, 5);
+  else if (nv == 2 && H == 10 && hc)
+    RDMI_PAIR(2, 10);
+  else if (nv == 1)
+    RDMI_PAIR(1, 0);
   else if (nv == 2)
-    RDMI_PAIR(2);
+    RDMI_PAIR(2, 0);
   else
-    RDMI_PAIR(3);
+    RDMI_PAIR(3, 0);
 #undef RDMI_PAIR
   return rdmi::check_launch("cross_attn_pair");
 }

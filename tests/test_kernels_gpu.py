@@ -489,9 +489,10 @@ def test_attention_smallkv():
 
 
 @pytest.mark.parametrize("M,C,H", [(999, 320, 5), (517, 640, 10), (64, 128, 2)])
-def test_cross_attn_pair(M, C, H):
+def test_cross_attn_pair(M, C, H, monkeypatch):
     """norm2 → attn2 (two-token context) → +residual as one row pass (rdmi_cross_attn_pair, exact
-    fold of the two-key softmax) against the unfolded fp32 computation of the reference block."""
+    fold of the two-key softmax) against the unfolded fp32 computation of the reference block; the
+    head-unrolled kernel (H = 5 / 10) bitwise the per-head loop (RDMI_PAIR_HC=0)."""
     K_ = _k()
     g = torch.Generator(device=DEV).manual_seed(31)
     x = torch.randn(M, C, device=DEV, generator=g).half()
@@ -503,7 +504,11 @@ def test_cross_attn_pair(M, C, H):
     ctx = torch.randn(2, C, device=DEV, generator=g).half()
     k2 = (ctx.float() @ wk.half().float().t()).half()
     v2 = (ctx.float() @ wv.half().float().t()).half()
-    y = K_.cross_attn_pair(x, lg, lb, 1e-5, *K_.fold_attn2_pair(wq, wo, bo, k2, v2, H))
+    fold = K_.fold_attn2_pair(wq, wo, bo, k2, v2, H)
+    y = K_.cross_attn_pair(x, lg, lb, 1e-5, *fold)
+    monkeypatch.setenv("RDMI_PAIR_HC", "0")
+    assert torch.equal(K_.cross_attn_pair(x, lg, lb, 1e-5, *fold), y)
+    monkeypatch.delenv("RDMI_PAIR_HC")
     n2 = F.layer_norm(x.float(), (C,), lg, lb, 1e-5)
     q = n2 @ wq.t()
     o = _sdpa_ref(q.half()[None], k2[None], v2[None], H)[0]
