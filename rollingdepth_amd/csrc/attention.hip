@@ -829,16 +829,48 @@ __global__ __launch_bounds__(256) void softmax_rows_reg_k(const float* __restric
 // weights, the output row — one read and one write of the row instead of LN + q GEMM + attention
 // + out GEMM (five row passes).  w, u, c are folded once per context (unet.Transformer).
 // HC > 0: H = HC at compile time — the H head dot products are formed first and their wave sums
-// run level by level together (H independent shuffle chains in flight instead of H serial ones), then
+// run level by level together (H independent reduction chains in flight instead of H serial ones), then
 // the sigmoids and the output accumulation in head order: the same operations on every value as the
 // HC = 0 loop, bitwise its output (the per-row latency of 2 + H dependent reductions was the bound:
 // ≈1.75 TB/s at C = 320, 0.9 at 640).
+// wave_sum's xor butterfly (32, 16, 8, 4, 2, 1: the same pairs, the same operand per add, so the
+// same bits) without the LDS crossbar: xor 32 / 16 as v_permlane32_swap / v_permlane16_swap of the
+// value with a copy of itself (the two results sum to v_i + v_partner in every lane), xor 8 as DPP
+// row_ror:8, xor 4 as row_ror:4 or row_ror:12 by lane bit 2 (b2 = (lane >> 2) & 1), xor 2 / 1 as
+// quad_perm — no ds_bpermute and no lgkmcnt wait in the chain (bitwise: tests/test_kernels_gpu.py
+// test_cross_attn_pair against the per-head shuffle loop).  The swaps are inline asm: hipcc folded the
+// builtins' swap of a value with itself into an identity (r0 + r1 = 2v); the s_nops cover the
+// VALU-write → permlane-read and permlane-write → VALU-read hazards.
+template <bool X32>
+__device__ __forceinline__ float swap_sum(float v) {
+  float a = v, b = v;
+  if constexpr (X32)
+    asm("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  else
+    asm("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  return a + b;
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 template <int HC>
-__device__ __forceinline__ void wave_sum_n(float (&d)[HC]) {
+__device__ __forceinline__ void wave_sum_n(float (&d)[HC], bool b2) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
+  for (int h = 0; h < HC; ++h) d[h] = swap_sum<true>(d[h]);
 #pragma unroll
-    for (int h = 0; h < HC; ++h) d[h] += __shfl_xor(d[h], o, 64);
+  for (int h = 0; h < HC; ++h) d[h] = swap_sum<false>(d[h]);
+#pragma unroll
+  for (int h = 0; h < HC; ++h) d[h] = d[h] + dppf<0x128>(d[h]);
+#pragma unroll
+  for (int h = 0; h < HC; ++h) {
+    const float p4 = dppf<0x124>(d[h]), p12 = dppf<0x12C>(d[h]);  // both read by every lane, then a select
+    d[h] = d[h] + (b2 ? p4 : p12);
+  }
+#pragma unroll
+  for (int h = 0; h < HC; ++h) d[h] = d[h] + dppf<0x4E>(d[h]);
+#pragma unroll
+  for (int h = 0; h < HC; ++h) d[h] = d[h] + dppf<0xB1>(d[h]);
 }
 
 template <int NV, int HC = 0>  // f16x8 vectors per lane: C ≤ 512·NV
@@ -855,6 +887,7 @@ __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f
   const float* ws = sm;
   const float* us = sm + H * C;
   const int lane = threadIdx.x & 63;
+  const bool b2 = (lane >> 2) & 1;
   const int CV = C >> 3;
   // this lane's columns are fixed: LN affine and the constant row c stay in registers
   float gr[NV][8], br[NV][8], cr[NV][8];
@@ -891,7 +924,9 @@ __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f
       if (lane + 64 * i < CV)
 #pragma unroll
         for (int e = 0; e < 8; ++e) s += (float)v[i][e];
-    const float mean = wave_sum(s) / C;
+    float sr[1] = {s};
+    if constexpr (HC > 0) wave_sum_n<1>(sr, b2); else sr[0] = wave_sum(s);
+    const float mean = sr[0] / C;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
@@ -901,7 +936,9 @@ __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f
           const float d = (float)v[i][e] - mean;
           q += d * d;
         }
-    const float rstd = rsqrtf(wave_sum(q) / C + eps);
+    float qr[1] = {q};
+    if constexpr (HC > 0) wave_sum_n<1>(qr, b2); else qr[0] = wave_sum(q);
+    const float rstd = rsqrtf(qr[0] / C + eps);
     float n[NV][8], o[NV][8];
 #pragma unroll
     for (int i = 0; i < NV; ++i)
@@ -925,7 +962,7 @@ __global__ __launch_bounds__(256) void attn2_pair_k(const f16* __restrict__ x, f
           }
         }
       }
-      wave_sum_n<HC>(d);
+      wave_sum_n<HC>(d, b2);
 #pragma unroll
       for (int h = 0; h < HC; ++h) {
         const float ph = 1.0f / (1.0f + __expf(-d[h]));
