@@ -128,15 +128,23 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
   const long total = nv * nb;
   const float* base = part + (long)(g * nv) * ld + (long)b * nb * 2;
   double S = 0.0, SS = 0.0;
-  // 8 independent loads in flight per thread, summed in the same per-thread order as one at a time
+  // 8 independent loads in flight per thread, summed in the same per-thread order as one at a time.
+  // Element i = v·nb + k: one 32-bit division per 8 elements, the rest stepped (a 64-bit division
+  // per element was most of this kernel's time — 25 µs a launch at the VAE's 768² shapes).
   constexpr int U = 8;
+  const unsigned nbu = (unsigned)nb;
   for (long i0 = t; i0 < total; i0 += 256 * U) {
     f32x2 e[U];
+    unsigned v = (unsigned)i0 / nbu, k = (unsigned)i0 - v * nbu;
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const long i = i0 + 256 * j;
-      const long v = i / nb, k = i - v * nb;
-      e[j] = i < total ? *(const f32x2*)(base + v * ld + k * 2) : f32x2{0.f, 0.f};
+      e[j] = i < total ? *(const f32x2*)(base + (long)v * ld + (long)k * 2) : f32x2{0.f, 0.f};
+      k += 256;
+      while (k >= nbu) {
+        k -= nbu;
+        ++v;
+      }
     }
 #pragma unroll
     for (int j = 0; j < U; ++j)

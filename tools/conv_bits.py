@@ -51,7 +51,9 @@ def main():
                         ("bm", dict(bias=bias, gn=True))):
             o3 = K.conv2d(x, w, co, 3, upsample=up, **kw)
             mom = getattr(o3, K._GN_ATTR, None)
-            print(f"ep{tag:5s} {lab:32s} {fp(o3)}" + (f" {fp(mom)}" if mom is not None else ""))
+            # GroupNorm statistics from the emitted moments (gn_from_partials) where they exist
+            st = f" {fp(K.groupnorm_stats(o3, 32, 1e-6))}" if mom is not None else ""
+            print(f"ep{tag:5s} {lab:32s} {fp(o3)}" + (f" {fp(mom)}" if mom is not None else "") + st)
     # implicit-GEMM (non-halo) conv modes: nearest-x2 upsample at 12 -> 24 (Ho % 16 != 0), stride 2
     for lab, B, H, ci, co, kw in [("up 1280 12->24", 4, 12, 1280, 1280, dict(upsample=True)),
                                   ("s2 320 96->48", 4, 96, 320, 320, dict(stride=2)),

@@ -72,6 +72,20 @@ def bench_conv1(iters):
         print(f"conv1 {lab:32s} {ms * 1e3:9.1f} us  {fl / ms / 1e9:8.1f} TFLOP/s {by / ms / 1e6:7.0f} GB/s")
 
 
+def bench_gnpart(iters):
+    """GroupNorm statistics from a producer's emitted moments (gn_from_partials) at the VAE / UNet shapes."""
+    for lab, B, H, C in [("vae 128 768^2 x9", 9, 768, 128), ("vae 256 384^2 x18", 18, 384, 256),
+                         ("vae 512 192^2 x36", 36, 192, 512), ("unet 640 48^2 x75", 75, 48, 640)]:
+        x = torch.randn(B, H, H, C, device="cuda").half()
+        w = K.pack_conv(torch.randn(C, C, 1, 1) / math.sqrt(C), "cuda", C)
+        o = K.conv2d(x, w, C, 1, pad=0, gn=True)
+        if getattr(o, K._GN_ATTR, None) is None:
+            print(f"gnpart {lab:30s} (no moments)")
+            continue
+        ms = timeit(lambda: K.groupnorm_stats(o, 32, 1e-6), iters)
+        print(f"gnpart {lab:30s} {ms * 1e3:9.1f} us")
+
+
 def bench_head(iters):
     """Decoder head: GroupNorm+SiLU+3x3 conv to one channel (rdmi_conv3x3_to1_gn)."""
     for B, H, C in [(16, 768, 128), (8, 768, 128)]:
@@ -307,4 +321,4 @@ if __name__ == "__main__":
     a = ap.parse_args()
     torch.manual_seed(0)
     for part in a.only.split(","):
-        {"attn512": bench_attn512, "conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "conv1": bench_conv1, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
+        {"attn512": bench_attn512, "conv": bench_conv, "gemm": bench_gemm, "attn": bench_attn, "gn": bench_gn, "gnconv": bench_gnconv, "head": bench_head, "conv1": bench_conv1, "gnpart": bench_gnpart, "sweep": bench_cinsweep, "sq": bench_square, "shapes": bench_shapes, "host": bench_host, "aligner": bench_aligner, "pair": bench_pair}[part](a.iters)
