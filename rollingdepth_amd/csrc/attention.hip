@@ -831,8 +831,9 @@ __global__ __launch_bounds__(256) void softmax_rows_reg_k(const float* __restric
 // HC > 0: H = HC at compile time — the H head dot products are formed first and their wave sums
 // run level by level together (H independent reduction chains in flight instead of H serial ones), then
 // the sigmoids and the output accumulation in head order: the same operations on every value as the
-// HC = 0 loop, bitwise its output (the per-row latency of 2 + H dependent reductions was the bound:
-// ≈1.75 TB/s at C = 320, 0.9 at 640).
+// HC = 0 loop, bitwise its output.  With the reductions below, 25-snippet L0 / L1 launches 476–497 →
+// 431 µs / 414 → 315 µs (profiles/r04ak_pair_dpp_ab.log); L0 stays vector-issue-bound (40 of 64 lanes
+// hold columns at C = 320).
 // wave_sum's xor butterfly (32, 16, 8, 4, 2, 1: the same pairs, the same operand per add, so the
 // same bits) without the LDS crossbar: xor 32 / 16 as v_permlane32_swap / v_permlane16_swap of the
 // value with a copy of itself (the two results sum to v_i + v_partner in every lane), xor 8 as DPP
