@@ -138,7 +138,10 @@ __global__ __launch_bounds__(HT) void head_taps_v(const T* __restrict__ x, long 
 //    one half of a register pair (op_sel) and does the two taps' FMAs, each rounding as v_fma_f32;
 //  * the butterfly's DPP moves fused into the adds (v_add_f32_dpp: 36 instructions, not 72);
 //  * the tap a lane writes picked by lane masks computed once (hipcc built a 9-way branch tree);
-//  * the next pixel's 16 bytes loaded before this pixel's arithmetic.
+//  * the next pixel's 16 bytes loaded before this pixel's arithmetic;
+//  * the taps written planar, d[t][B·HW], for head_gather (its 9 reads per output coalesced across
+//    lanes; the pixel-major d[p][9] made each read touch 64 pixels 36 B apart) — the same sums in the
+//    same order, so the same output bits.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int LO>  // acc.xy += y[LO] * w.xy
@@ -196,6 +199,7 @@ struct Head16 {
   float w8[8];     // tap 8
   int cl;
 
+  long P;  // planar tap stride: d[t][B·HW]
   __device__ __forceinline__ void pixel(const Raw8<T>& v, float* __restrict__ dq) const {
     f32x2 y[4];
 #pragma unroll
@@ -230,7 +234,7 @@ struct Head16 {
     o = cl == 6 ? s6 : o;
     o = cl == 7 ? s7 : o;
     o = cl == 8 ? a8 : o;
-    if (cl < 9) dq[cl] = o;  // tap cl written by lane cl of the group
+    if (cl < 9) dq[cl * P] = o;  // tap cl written by lane cl of the group, planar (head_gather)
   }
 };
 
@@ -260,18 +264,19 @@ __global__ __launch_bounds__(HT) void head_taps_16(const T* __restrict__ x, long
   long p = pbeg + threadIdx.x / LPP;
   if (p >= pend) return;
   const T* xb = x + (long)b * HW * C + c0;
-  float* db = d + (long)b * HW * 9;
+  float* db = d + (long)b * HW;
+  h.P = P;
   // two raw buffers in turn; the next pixel's load is unconditional (clamped to the last pixel) so
   // that the wait before each pixel's arithmetic counts only the older load
   Raw8<T> ra, rb;
   ra.load(xb + p * C);
   for (;;) {
     rb.load(xb + (p + S < pend ? p + S : pend - 1) * C);
-    h.pixel(ra, db + p * 9);
+    h.pixel(ra, db + p);
     p += S;
     if (p >= pend) break;
     ra.load(xb + (p + S < pend ? p + S : pend - 1) * C);
-    h.pixel(rb, db + p * 9);
+    h.pixel(rb, db + p);
     p += S;
     if (p >= pend) break;
   }
@@ -345,14 +350,19 @@ int head_launch(const void* x, int B, int H, int W, int C, int G, const float* m
                          beta, w, workspace, P, PPB);                                                            \
     break;
     switch (lpp) {
-      case 16:
+      case 16: {
         if (silu)
           hipLaunchKernelGGL((head_taps_16<T, true>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma, beta,
                              w, workspace, P, PPB);
         else
           hipLaunchKernelGGL((head_taps_16<T, false>), g, dim3(HT), 0, s, (const T*)x, HW, G, mean_rstd, gamma, beta,
                              w, workspace, P, PPB);
-        break;
+        int rc = rdmi::check_launch("conv3x3_to1_gn taps");
+        if (rc) return rc;
+        // planar taps: the gather's 9 reads per output are coalesced across lanes
+        hipLaunchKernelGGL(head_gather<U>, dim3(rdmi::div_up(P, HT)), dim3(HT), 0, s, workspace, H, W, P, bias, (U*)y);
+        return rdmi::check_launch("conv3x3_to1_gn gather");
+      }
       RDMI_HEAD(1) RDMI_HEAD(2) RDMI_HEAD(4) RDMI_HEAD(8) RDMI_HEAD(32) RDMI_HEAD(64)
       default: break;
     }
