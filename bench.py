@@ -190,6 +190,121 @@ def _validate(pipe, frames_dev, noise, dil0, snippet0, depth_host, coaligned_hos
     return info
 
 
+# Collective cost model for the rank-slice prediction (an assumption, stated with the numbers): RCCL over
+# xGMI, 7 links per MI355X; all-gathers and the merge all-to-all move each rank's share over several links
+# at once.  A deliberately conservative aggregate per GPU and a fixed cost per collective.
+SLICE_XGMI_GBS = 100.0
+SLICE_COLL_US = 50.0
+
+
+def _slice_main(a) -> int:
+    """bench.py --slice-world W[,W..]: for each W and each rank r < W, run exactly rank r's work of the
+    W-rank strong-scaling forward (shard.sharded_forward with shard.SliceGroup: its encode chunk, its
+    snippets' UNet steps and decodes, the replicated aligner, its windowed partial merge, its egress;
+    collectives replaced by local no-ops) on this one GPU, timed per phase with HIP events; beside it the
+    single-GPU step of the same preset.  Prints one JSON line per W: per-rank step times, phases, the
+    predicted W-GPU step = max over ranks + a collective model (SLICE_XGMI_GBS, SLICE_COLL_US), and the
+    predicted efficiency T1 / (W · T_W).  Not a scaling number: nothing here ran on W GPUs."""
+    import torch
+
+    from rollingdepth_amd import config as C
+    from rollingdepth_amd import weights as W
+    from rollingdepth_amd.pipeline import RollingDepthPipeline
+    from rollingdepth_amd.shard import SliceGroup, chunk_bounds, merge_exchange_plan, rank_subsets, sharded_forward
+
+    pr = dict(PRESETS[a.preset])
+    res = a.res or pr["res"]
+    dil0 = [int(x) for x in a.dilations.split(",")] if a.dilations else list(pr["dilations"])
+    N = a.frames_total or pr["frames_total"]
+    dev = torch.device("cuda", 0)
+    tdt = torch.float32 if pr["dtype"] == "f32" else torch.float16
+    pipe = RollingDepthPipeline.from_synthetic(C.SD2_UNET, C.SD2_VAE, C.RD_SCHEDULER, device=dev, torch_dtype=tdt)
+    pipe.snippet_batch = a.snippet_batch
+    pipe.vae_batch = a.vae_batch
+    frames_all = W.synth_frames(N, res, res, seed=0)
+    noise = W.synth_noise(res // 8, res // 8).to(dev)
+    coalign = {"num_iterations": a.aligner_iters}
+    refine = pr["refine"]
+
+    # single-GPU reference step (the same forward bench.py times at N = 1)
+    f1dev = frames_all[None].to(dev, tdt)
+
+    def one():
+        pipe.forward(f1dev, list(dil0), pr["cap"], [3], [1], [1], coalign, refine, 3, 6, None, False, 4, False,
+                     init_noise=noise)
+
+    for _ in range(a.warmup):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one()
+    torch.cuda.synchronize()
+    t1 = (time.perf_counter() - t0) / a.steps
+    del f1dev
+    print(f"single-GPU step {t1 * 1e3:.1f} ms ({N / t1:.2f} depth frames/s)", flush=True)
+
+    dil = [pipe.cap_max_dilation(N, 3, d) for d in dil0] if pr["cap"] else list(dil0)
+    counts = [len(pipe.get_snippet_indice(0, [0], N, 3, d, d, 1)) for d in dil]
+    h = res // 8
+    P = ((res - 4 + 9) // 10) ** 2  # aligner inputs: border 2, every 10th pixel (depth_aligner.py:82-92)
+    for Wd in [int(x) for x in a.slice_world.split(",")]:
+        ranks = []
+        for r in range(Wd):
+            lo, hi = chunk_bounds(N, Wd)[r]
+            fr = frames_all[lo:hi].to(dev, tdt)
+            g = SliceGroup(r, Wd)
+
+            def step(timing=None):
+                sharded_forward(pipe, fr, list(dil0), pr["cap"], 3, coalign, init_noise=noise, num_frames=N,
+                                to_host=True, refine_step=refine, group=g, timing=timing)
+
+            for _ in range(a.warmup):
+                step()
+            torch.cuda.synchronize()
+            phases, walls = {}, []
+            for _ in range(a.steps):
+                tm = []
+                ts = time.perf_counter()
+                step(tm)
+                torch.cuda.synchronize()
+                walls.append(time.perf_counter() - ts)
+                for (n0, e0), (n1, e1) in zip(tm, tm[1:]):
+                    phases[n1] = phases.get(n1, 0.0) + e0.elapsed_time(e1) / a.steps
+            sub = rank_subsets(counts, Wd, r)
+            rng_, send, recv = merge_exchange_plan(counts, dil, [3] * len(dil), N, Wd, r)
+            nrecv = [sum(m for _, m in pc) for pc in recv]
+            ranks.append({"rank": r, "ms": round(statistics.median(walls) * 1e3, 1),
+                          "phases_ms": {k: round(v, 1) for k, v in phases.items()},
+                          "frames": hi - lo, "snippets": [len(x) for x in sub], "merge_frames": rng_,
+                          "merge_rows_sent": sum(send) - send[r], "merge_rows_recv": sum(nrecv) - nrecv[r]})
+            del fr
+            print(f"W={Wd} rank {r}: {ranks[-1]['ms']} ms {ranks[-1]['phases_ms']}", flush=True)
+        # collective model: latents + aligner-input all-gathers, the merge all-to-all, two min/max all-reduces
+        esz = 2 if tdt == torch.float16 else 4
+        lat_b = (Wd - 1) / Wd * N * h * h * 8 * esz
+        ali_b = (Wd - 1) / Wd * sum(counts) * 3 * P * 4
+        m_rows = max(max(x["merge_rows_sent"], x["merge_rows_recv"]) for x in ranks)
+        merge_b = m_rows * res * res * 8
+        n_coll = 5 + (2 * refine if refine else 0)
+        ref_b = (2 * (Wd - 1) / Wd * N * h * h * 4 * 8 * refine + (Wd - 1) / Wd * N * h * h * 8 * esz) if refine else 0
+        comm_s = (lat_b + ali_b + merge_b + ref_b) / (SLICE_XGMI_GBS * 1e9) + n_coll * SLICE_COLL_US * 1e-6
+        tmax = max(x["ms"] for x in ranks) * 1e-3
+        tw = tmax + comm_s
+        line = {"mode": "rank-slice", "note": "not a scaling number: each rank's share of a W-rank run timed "
+                                              "alone on one GPU, collectives modelled",
+                "preset": a.preset, "frames": N, "res": res, "dilations": dil, "world": Wd,
+                "single_gpu_ms": round(t1 * 1e3, 1), "ideal_ms": round(t1 / Wd * 1e3, 1),
+                "max_rank_ms": round(tmax * 1e3, 1), "comm_model_ms": round(comm_s * 1e3, 2),
+                "comm_model": f"{SLICE_XGMI_GBS:.0f} GB/s per GPU + {SLICE_COLL_US:.0f} us per collective: "
+                              f"latents {lat_b / 1e6:.1f} MB, aligner inputs {ali_b / 1e6:.1f} MB, merge "
+                              f"{merge_b / 1e6:.1f} MB, refine {ref_b / 1e6:.1f} MB",
+                "predicted_ms": round(tw * 1e3, 1), "predicted_efficiency": round(t1 / (Wd * tw), 4),
+                "predicted_depth_frames_per_s": round(N / tw, 2), "ranks": ranks}
+        print(json.dumps(line), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,7 +323,12 @@ def main():
     ap.add_argument("--cpu-768-runs", type=int, default=1)
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--aligner-iters", type=int, default=2000)
+    ap.add_argument("--slice-world", default=None,
+                    help="e.g. 2,4,8: on ONE GPU, time each rank's share of a W-rank run (collectives as local "
+                         "no-ops, shard.SliceGroup) beside the single-GPU step — not a scaling number")
     a = ap.parse_args()
+    if a.slice_world:
+        sys.exit(_slice_main(a))
 
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and a.gpus > 1:

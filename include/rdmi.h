@@ -239,7 +239,8 @@ int rdmi_ddim_combine(const void* x, long ld_x, const void* e, long ld_e, void* 
                       int dtype, void* stream);
 /* Refine averaging (rollingdepth_pipeline.py:586-629): out[f] = mean over the snippets s = f − j·stride
  * (0 ≤ s < n) of src[s][j]; src [n][w][P][ld], out [N][P][ld] f16 (channels ≥ C zeroed).  The sum is
- * taken in f64 (exact for these few f32 terms, hence independent of the order of addition). */
+ * taken in f64: exact for f16 terms (hence independent of the order of addition); for f32 terms
+ * order-independent except when the terms' exponents span more than ≈29 bits (rare). */
 int rdmi_snippet_average(const void* src, int n, int w, int stride, int N, long P, int C, int ld,
                          void* out, int dtype, void* stream);
 /* Depth colourisation (src/util/colorize.py:12-93, the CLI's visualisation): rgb [n][3] u8 =
@@ -254,8 +255,9 @@ int rdmi_colorize(const void* depth, int dtype, long n, const void* minmax, cons
  * per frame the sum over THIS rank's snippets k0 .. k0+nloc-1 (src [nloc][w][P][ld], dtype RDMI_F16 /
  * RDMI_F32), zero where none covers the frame; after an all-reduce SUM over ranks,
  * rdmi_snippet_finish divides by the frame's cover count over all n snippets → out [N][P][ld]
- * (channels ≥ C zeroed).  The f64 sums are exact, so every world size and every all-reduce order
- * reproduces rdmi_snippet_average bitwise. */
+ * (channels ≥ C zeroed).  The f64 sums are exact for f16 terms, so every world size and every
+ * all-reduce order reproduces rdmi_snippet_average bitwise; with f32 terms the same holds except in rare
+ * rounding cases (terms whose exponents span more than ≈29 bits). */
 int rdmi_snippet_accumulate(const void* src, int dtype, int k0, int nloc, int w, int stride, int N, long P, int C,
                             int ld, double* sum, void* stream);
 int rdmi_snippet_finish(const double* sum, int n, int w, int stride, int N, long P, int C, int ld, void* out,
@@ -309,14 +311,29 @@ int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float*
  * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w_d][HW] — into sum_out [seq_len][HW] f64 (the
  * same per-slot arithmetic as rdmi_aligner_merge, zero where no local slot covers a frame); after a
  * reduce-scatter SUM by frame, rdmi_aligner_merge_finish divides frames f0 .. f0+nf-1 by their cover
- * count over all n[d] snippets.  With f32 arithmetic (x_f32 1 / 2) the f64 sums are exact, so any world
- * size and reduction order reproduces rdmi_aligner_merge bitwise. */
+ * count over all n[d] snippets.  With f32 arithmetic (x_f32 1 / 2) the f64 sums are order-independent
+ * (exact while a frame's terms span ≤ ≈29 exponent bits, i.e. except in rare rounding cases), so any
+ * world size and reduction order reproduces rdmi_aligner_merge bitwise in practice. */
 int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                const float* const* t, const int* n, const int* stride, const int* k0,
                                const int* nloc, const int* w, int seq_len, long HW, const float* shift, double* sum_out,
                                void* stream);
 int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf, long HW,
                               const double* sum, float* out, void* stream);
+/* Sharded merge over frame windows (round 5; replaces the full [seq_len, HW] reduce-scatter): each rank
+ * sums only frames f0 .. f0+nf-1 — the window its own snippets cover — into sum_out [nf][HW] f64 (the
+ * arithmetic of rdmi_aligner_merge_partial), sends every other rank the rows of that rank's frame chunk
+ * (an all-to-all of uneven row counts), and rdmi_aligner_merge_finish_pieces adds the received pieces per
+ * frame in source-rank order and divides by the frame's cover count: piece q = frames piece_f0[q] ..
+ * piece_f0[q]+piece_nf[q]-1 of one source, pieces stored back to back in recv [Σ piece_nf][HW] f64, all
+ * inside this rank's frames f0 .. f0+nf-1 (≤ 64 pieces) → out [nf][HW] f32. */
+int rdmi_aligner_merge_partial_window(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                                      const float* const* t, const int* n, const int* stride, const int* k0,
+                                      const int* nloc, const int* w, int f0, int nf, long HW, const float* shift,
+                                      double* sum_out, void* stream);
+int rdmi_aligner_merge_finish_pieces(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf, long HW,
+                                     int npieces, const int* piece_f0, const int* piece_nf, const double* recv,
+                                     float* out, void* stream);
 
 /* Single-head flash attention for head dim 512 (f16): the VAE mid-block attention
  * (unet_2d_blocks.py:680-697 through AttnProcessor2_0's 4-D path, attention_processor.py:2172-2276 —

@@ -106,6 +106,11 @@ _SIGS = {
                                          vp, vp, vp]),
     "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64, vp, vp,
                                         vp]),
+    "rdmi_aligner_merge_partial_window": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp),
+                                                C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
+                                                C.POINTER(i32), i32, i32, i64, vp, vp, vp]),
+    "rdmi_aligner_merge_finish_pieces": (i32, [i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64,
+                                               i32, C.POINTER(i32), C.POINTER(i32), vp, vp, vp]),
 }
 
 RDMI_F16, RDMI_F32, RDMI_U8, RDMI_F32_X3 = 0, 1, 2, 3

@@ -449,8 +449,8 @@ __device__ __forceinline__ int cover_count(const int* n, const int* stride, int 
 }
 
 // The f32-arithmetic merges (x_f32 1 / 2) add the slots' f32 terms s·x + t in f64: the sum of a
-// frame's few (≤ Σ w_d) f32 terms is then exact, so it does not depend on the order the terms are
-// added in — the sharded merge (per-rank partial sums, reduce-scatter in RCCL's order, finish)
+// frame's few (≤ Σ w_d) f32 terms is exact whenever their exponents span ≤ ≈29 bits (all but rare
+// rounding cases), so it does not depend on the order the terms are added in — the sharded merge (per-rank partial sums, reduce-scatter in RCCL's order, finish)
 // gives bitwise the single-GPU result, and both round once, at the mean.  The f16-emulating mode 0
 // (the reference's fp16 merge, RDMI_MERGE_F32=0) keeps its f32 running sum.
 __global__ void merge_k(MergeP p) {
@@ -501,6 +501,28 @@ __global__ void merge_finish_k(MergeP p, const double* __restrict__ sum) {
   for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
     const long i = (long)fl * p.HW + px;
     p.out[i] = cnt ? (float)(sum[i] / (double)cnt) : 0.f;
+  }
+}
+
+// sharded merge with frame windows, second half: the received pieces — piece q holds the sums of
+// frames pf0[q] .. pf0[q]+pnf[q]-1 from one source rank, pieces back to back in `recv` — added per
+// frame in piece (= source rank) order, ÷ the frame's cover count.  Frames of this rank's chunk that
+// no piece covers are 0 (no slot covers them: cover count 0).
+constexpr int MAXPIECES = 64;
+struct PiecesP {
+  int pf0[MAXPIECES], pnf[MAXPIECES];
+  long poff[MAXPIECES];
+  int np;
+};
+
+__global__ void merge_finish_pieces_k(MergeP p, PiecesP q, const double* __restrict__ recv) {
+  const int fl = blockIdx.y, f = p.f0 + fl;
+  const int cnt = cover_count(p.n, p.stride, p.nd, p.w, f);
+  for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int i = 0; i < q.np; ++i)
+      if (f >= q.pf0[i] && f < q.pf0[i] + q.pnf[i]) s += recv[q.poff[i] + (long)(f - q.pf0[i]) * p.HW + px];
+    p.out[(long)fl * p.HW + px] = cnt ? (float)(s / (double)cnt) : 0.f;
   }
 }
 
@@ -700,6 +722,45 @@ extern "C" int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int 
                                           double* sum_out, void* stream) {
   RDMI_REQUIRE(k0 && nloc && sum_out, RDMI_E_ARG, "aligner_merge_partial: k0/nloc/sum_out required");
   return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, 0, seq_len, HW, shift, nullptr, sum_out, stream);
+}
+
+extern "C" int rdmi_aligner_merge_partial_window(int n_dil, const void* const* xf, int x_f32, const float* const* s,
+                                                 const float* const* t, const int* n, const int* stride, const int* k0,
+                                                 const int* nloc, const int* w, int f0, int nf, long HW,
+                                                 const float* shift, double* sum_out, void* stream) {
+  RDMI_REQUIRE(k0 && nloc && sum_out, RDMI_E_ARG, "aligner_merge_partial_window: k0/nloc/sum_out required");
+  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, f0, nf, HW, shift, nullptr, sum_out, stream);
+}
+
+extern "C" int rdmi_aligner_merge_finish_pieces(int n_dil, const int* n, const int* stride, const int* w, int f0,
+                                                int nf, long HW, int npieces, const int* piece_f0,
+                                                const int* piece_nf, const double* recv, float* out, void* stream) {
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && out && HW > 0 && f0 >= 0 && nf >= 0 &&
+                   npieces >= 0 && npieces <= MAXPIECES && (npieces == 0 || (piece_f0 && piece_nf && recv)),
+               RDMI_E_ARG, "aligner_merge_finish_pieces: bad args");
+  if (nf == 0) return 0;
+  MergeP p{};
+  for (int d = 0; d < n_dil; ++d) {
+    p.n[d] = n[d];
+    p.stride[d] = stride[d];
+    p.w[d] = w[d];
+  }
+  p.nd = n_dil; p.HW = HW; p.out = out; p.f0 = f0;
+  PiecesP q{};
+  long off = 0;
+  for (int i = 0; i < npieces; ++i) {
+    RDMI_REQUIRE(piece_nf[i] >= 0 && piece_f0[i] >= f0 && piece_f0[i] + piece_nf[i] <= f0 + nf, RDMI_E_ARG,
+                 "aligner_merge_finish_pieces: piece %d frames %d+%d outside %d+%d", i, piece_f0[i], piece_nf[i], f0, nf);
+    q.pf0[i] = piece_f0[i];
+    q.pnf[i] = piece_nf[i];
+    q.poff[i] = off;
+    off += (long)piece_nf[i] * HW;
+  }
+  q.np = npieces;
+  long gx = (HW + 255) / 256;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(merge_finish_pieces_k, dim3((unsigned)gx, nf), dim3(256), 0, (hipStream_t)stream, p, q, recv);
+  return rdmi::check_launch("aligner_merge_finish_pieces");
 }
 
 extern "C" int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf,

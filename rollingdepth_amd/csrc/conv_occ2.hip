@@ -31,7 +31,8 @@ void launch_conv_h32(bool gn, dim3 g, hipStream_t s, const GemmP& p) {
 }
 
 void launch_gemm_occ2(int bn, dim3 g, hipStream_t s, const GemmP& p) {
-  if (bn == 160)
+  // bn == 160 never carries GEGLU (launch_mode): its epilogue exists only for 64-column waves
+  if (bn == 160 && !p.geglu)
     hipLaunchKernelGGL((gemm_occ2_kernel<0, 160>), g, dim3(256), 0, s, p);
   else
     hipLaunchKernelGGL((gemm_occ2_kernel<0, 128>), g, dim3(256), 0, s, p);

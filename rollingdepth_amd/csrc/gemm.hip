@@ -50,9 +50,10 @@ void launch_mode(const GemmP& p, int batch, hipStream_t s, bool force128) {
     const int oc = occ2_mode();
     const bool pick = !p.geglu && batch == 1 && !p.c_f32 && p.N <= 1920 && p.N % 128 != 0;
     if (oc == 2 || (oc == 1 && pick)) {
-      // 160-column tiles where N allows (RDMI_GEMM_BN160=0: 128 only, for A/B)
+      // 160-column tiles where N allows (RDMI_GEMM_BN160=0: 128 only, for A/B).  GEGLU stays on
+      // 128-column tiles: its epilogue exists only for 64-column waves (store_tile_t)
       const char* e160 = getenv("RDMI_GEMM_BN160");
-      const int bn = (p.N % 160 == 0 && !(e160 && e160[0] == '0')) ? 160 : 128;
+      const int bn = (p.N % 160 == 0 && !p.geglu && !(e160 && e160[0] == '0')) ? 160 : 128;
       dim3 g(rdmi::div_up(p.N, bn), rdmi::div_up(p.M, 128), batch);
       launch_gemm_occ2(bn, g, s, p);
       return;

@@ -133,6 +133,8 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
   // per element was most of this kernel's time — 25 µs a launch at the VAE's 768² shapes).
   constexpr int U = 8;
   const unsigned nbu = (unsigned)nb;
+  // a step of 256 elements = dq whole rows of nb + dr: one compare per element whatever nb is
+  const unsigned dq = 256u / nbu, dr = 256u % nbu;
   for (long i0 = t; i0 < total; i0 += 256 * U) {
     f32x2 e[U];
     unsigned v = (unsigned)i0 / nbu, k = (unsigned)i0 - v * nbu;
@@ -140,8 +142,9 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
     for (int j = 0; j < U; ++j) {
       const long i = i0 + 256 * j;
       e[j] = i < total ? *(const f32x2*)(base + (long)v * ld + (long)k * 2) : f32x2{0.f, 0.f};
-      k += 256;
-      while (k >= nbu) {
+      k += dr;
+      v += dq;
+      if (k >= nbu) {
         k -= nbu;
         ++v;
       }

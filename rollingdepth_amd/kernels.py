@@ -5,7 +5,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import os
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -884,6 +884,49 @@ def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int
     stv = (C.c_int * nd)(*list(strides))
     check(lib.rdmi_aligner_merge_partial(nd, xp, int(x_f32), sp, tp, nn, stv, kk, nl, wv, seq_len, HW,
                                          shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge_partial")
+    return out
+
+
+def aligner_merge_partial_window(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int], n: Sequence[int], scales,
+                                 trans, strides, w: Sequence[int], f0: int, nf: int, HW: int, shift: torch.Tensor,
+                                 x_f32, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """aligner_merge_partial restricted to frames f0 .. f0+nf-1 (a range the rank's snippets cover)
+    → f64 [nf, HW] (`out`: a contiguous f64 [nf, HW] view to write into)."""
+    nd = len(xf)
+    if out is None:
+        out = torch.empty((nf, HW), dtype=torch.float64, device=shift.device)
+    elif out.dtype != torch.float64 or tuple(out.shape) != (nf, HW) or not out.is_contiguous():
+        raise ValueError("aligner_merge_partial_window: out must be contiguous f64 [nf, HW]")
+    xp = (C.c_void_p * nd)(*[(x.data_ptr() if x is not None and x.shape[0] else None) for x in xf])
+    sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
+    tp = (C.c_void_p * nd)(*[t.data_ptr() for t in trans])
+    nn = (C.c_int * nd)(*list(n))
+    kk = (C.c_int * nd)(*list(k0))
+    nl = (C.c_int * nd)(*[(x.shape[0] if x is not None else 0) for x in xf])
+    stv = (C.c_int * nd)(*list(strides))
+    wv = (C.c_int * nd)(*list(w))
+    check(lib.rdmi_aligner_merge_partial_window(nd, xp, int(x_f32), sp, tp, nn, stv, kk, nl, wv, f0, nf, HW,
+                                                shift.data_ptr(), out.data_ptr(), _stream()),
+          "rdmi_aligner_merge_partial_window")
+    return out
+
+
+def aligner_merge_finish_pieces(recv: torch.Tensor, pieces: Sequence[Tuple[int, int]], n: Sequence[int],
+                                strides: Sequence[int], w: Sequence[int], f0: int, nf: int, HW: int) -> torch.Tensor:
+    """Sharded merge over frame windows, after the all-to-all: recv f64 [Σ nf_q, HW] = the pieces
+    (first frame, frame count) back to back in source-rank order → f32 [nf, HW] means of frames f0 .."""
+    if recv.dtype != torch.float64:
+        raise TypeError("aligner_merge_finish_pieces: f64 sums expected")
+    nd, npc = len(n), len(pieces)
+    out = torch.empty((nf, HW), dtype=F32, device=recv.device)
+    nn = (C.c_int * nd)(*list(n))
+    stv = (C.c_int * nd)(*list(strides))
+    wv = (C.c_int * nd)(*list(w))
+    pf = (C.c_int * max(npc, 1))(*[p[0] for p in pieces])
+    pn = (C.c_int * max(npc, 1))(*[p[1] for p in pieces])
+    check(lib.rdmi_aligner_merge_finish_pieces(nd, nn, stv, wv, f0, nf, HW, npc, pf, pn,
+                                               recv.data_ptr() if recv.numel() else None, out.data_ptr(),
+                                               _stream()), "rdmi_aligner_merge_finish_pieces")
     return out
 
 

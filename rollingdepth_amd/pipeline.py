@@ -397,8 +397,8 @@ class RollingDepthPipeline:
         step's averaged latents."""
         world, rank = 1, 0
         if group is not None:
-            import torch.distributed as dist
-            world, rank = dist.get_world_size(group), dist.get_rank(group)
+            from .shard import _rank, _world
+            world, rank = _world(group), _rank(group)
         self._context()
         N, h, w, _ = rgb_latent.shape
         T = int(refine_step / skip_t_ratio)

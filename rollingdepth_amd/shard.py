@@ -24,9 +24,10 @@ Outputs stay distributed: rank r holds depth / coaligned depth for frames chunk_
 (and its own decoded snippets); `gather=True` assembles the full maps on every rank.
 
 Numerics vs the single-GPU forward: identical per-snippet arithmetic.  The cross-rank sums — the
-merge of s·x+t per frame and refine's per-frame average of snippet predictions — are exact f64 sums
-of f32 terms on both paths (aligner.hip merge_k, elementwise.hip snippet_*), so the order RCCL
-reduces them in does not change a bit; the aligner runs the same kernel on the same (all-gathered)
+merge of s·x+t per frame and refine's per-frame average of snippet predictions — are f64 sums on
+both paths (aligner.hip merge_k, elementwise.hip snippet_*): exact for f16 terms, and for f32 terms
+exact unless a frame's terms span more than ≈29 exponent bits (rare), so the order RCCL reduces them
+in does not change a bit in practice; the aligner runs the same kernel on the same (all-gathered)
 inputs.  What can still differ is the kernel engine chosen per launch shape (the f32 accumulation
 order inside a conv / GEMM depends on the batch a rank runs), which at SD2 shapes is not bitwise.
 Stated tolerance: depth mean |Δ| ≤ 1e-3 (the north_star bound) against the single-GPU result
@@ -65,6 +66,27 @@ def rank_subsets(counts: Sequence[int], world: int, rank: int) -> List[List[int]
     return sub
 
 
+class SliceGroup:
+    """Stand-in process group for timing ONE rank's share of a W-rank run on one GPU (bench.py
+    --slice-world): the rank runs exactly its own encode chunk, snippets, decode, aligner and partial
+    merge, and every collective is a local no-op that fills the received buffers with this rank's own
+    data (so the kernels after it see data of the same shape and range).  Not a scaling measurement:
+    it leaves out the collectives' time and overlap."""
+
+    def __init__(self, rank: int, world: int):
+        if not 0 <= rank < world:
+            raise ValueError(f"slice rank {rank} of world {world}")
+        self.rank, self.world = rank, world
+
+
+def _rank(group) -> int:
+    return group.rank if isinstance(group, SliceGroup) else dist.get_rank(group)
+
+
+def _world(group) -> int:
+    return group.world if isinstance(group, SliceGroup) else dist.get_world_size(group)
+
+
 def _via_host(group, t: torch.Tensor) -> bool:
     """gloo has no device transport: device tensors are staged through host memory (tests that run
     several ranks on one GPU, or CPU ranks); RCCL moves device memory directly over xGMI."""
@@ -72,6 +94,9 @@ def _via_host(group, t: torch.Tensor) -> bool:
 
 
 def _gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
+    if isinstance(group, SliceGroup):  # every rank's slot gets this rank's rows
+        out.view(-1, inp.numel()).copy_(inp.reshape(1, -1).expand(out.numel() // max(inp.numel(), 1), -1))
+        return
     if _via_host(group, inp):
         o = out.cpu()
         dist.all_gather_into_tensor(o, inp.cpu(), group=group)
@@ -81,6 +106,8 @@ def _gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
 
 
 def _all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
+    if isinstance(group, SliceGroup):
+        return
     if _via_host(group, t):
         h = t.cpu()
         dist.all_reduce(h, op=op, group=group)
@@ -108,19 +135,23 @@ def _reduce_scatter_rows(full: torch.Tensor, world: int, group=None) -> torch.Te
         full = torch.cat([full, torch.zeros((c * world - total, *full.shape[1:]), dtype=full.dtype,
                                             device=full.device)])
     out = torch.empty((c, *full.shape[1:]), dtype=full.dtype, device=full.device)
-    if _via_host(group, full):
+    if isinstance(group, SliceGroup):
+        out.copy_(full[group.rank * c:(group.rank + 1) * c])
+    elif _via_host(group, full):
         o = out.cpu()
         dist.reduce_scatter_tensor(o, full.contiguous().cpu(), group=group)
         out.copy_(o)
     else:
         dist.reduce_scatter_tensor(out, full.contiguous(), group=group)
-    rank = dist.get_rank(group)
+    rank = _rank(group)
     lo, hi = chunk_bounds(total, world)[rank]
     return out[:hi - lo]
 
 
 def _broadcast(t: torch.Tensor, src: int = 0, group=None):
     """Broadcast from the group's rank `src` (device tensors staged through the host under gloo)."""
+    if isinstance(group, SliceGroup):
+        return
     root = dist.get_global_rank(group, src) if group is not None and group != dist.group.WORLD else src
     if _via_host(group, t):
         h = t.cpu()
@@ -142,7 +173,7 @@ def gather_rows_by_dilation(local: Sequence[torch.Tensor], counts: Sequence[int]
     plan = [rank_subsets(counts, world, r) for r in range(world)]
     per_rank = [sum(len(sub[d]) * sizes[d] for d in range(len(counts))) for sub in plan]
     cap = max(max(per_rank), 1)
-    rank = dist.get_rank(group)
+    rank = _rank(group)
     for d, t in enumerate(local):
         if t.shape[0] != len(plan[rank][d]):
             raise ValueError(f"rank {rank} holds {t.shape[0]} rows of dilation {d}, its plan {len(plan[rank][d])}")
@@ -170,6 +201,94 @@ def _all_reduce_minmax(mm: torch.Tensor, group=None) -> torch.Tensor:
     return torch.stack([t[0], -t[1]])
 
 
+def frame_ranges(subsets: Sequence[Sequence[int]], strides: Sequence[int], w: Sequence[int]) -> List[Tuple[int, int]]:
+    """Frames a rank's snippets cover, as sorted disjoint ranges [lo, hi): slot j of snippet k of
+    dilation d is frame k + j·stride_d (depth_aligner.py:179-188); one range per dilation's contiguous
+    snippet run (a dilation's frames between its slots included), overlapping ranges joined."""
+    rs = sorted((min(sub), max(sub) + (wd - 1) * st + 1) for sub, st, wd in zip(subsets, strides, w) if sub)
+    out: List[Tuple[int, int]] = []
+    for lo, hi in rs:
+        if out and lo <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], hi))
+        else:
+            out.append((lo, hi))
+    return out
+
+
+def _cut(ranges: Sequence[Tuple[int, int]], lo: int, hi: int) -> List[Tuple[int, int]]:
+    """Parts of `ranges` inside [lo, hi) as (first frame, frame count), in order."""
+    return [(max(a, lo), min(b, hi) - max(a, lo)) for a, b in ranges if min(b, hi) > max(a, lo)]
+
+
+def merge_exchange_plan(counts: Sequence[int], strides: Sequence[int], w: Sequence[int], N: int, world: int,
+                        rank: int):
+    """The all-to-all of the windowed merge, from the plan alone (no communication): this rank's
+    frame ranges, the rows it sends to each rank (its rows inside that rank's frame chunk — the
+    ranges' rows are stored in frame order, so each destination's rows are contiguous) and the pieces
+    (first frame, frame count) it receives from each rank (the sender's ranges cut by this rank's
+    chunk, in frame order)."""
+    ranges = [frame_ranges(rank_subsets(counts, world, r), strides, w) for r in range(world)]
+    chunks = chunk_bounds(N, world)
+    send = [sum(m for _, m in _cut(ranges[rank], *chunks[r])) for r in range(world)]
+    recv = [_cut(ranges[r], *chunks[rank]) for r in range(world)]
+    return ranges[rank], send, recv
+
+
+def _merge_windowed(rows, k0, counts, scales, trans, strides, slens, N: int, HW: int, shift, x_f32, group):
+    """merge_scaled_triplets over W ranks: per-rank f64 sums of only the frames its snippets cover, an
+    all-to-all of the rows each rank's frame chunk needs (uneven row counts; RCCL over xGMI), then
+    the received pieces added per frame in source-rank order and ÷ the cover count (f64 sums: the
+    single-GPU merge bitwise, as the full reduce-scatter it replaces).  Returns this rank's chunk
+    [f1 − f0, HW] f32.  Moves each rank's covered frames instead of N·HW·8 B per rank."""
+    from . import kernels as K
+
+    world, rank = _world(group), _rank(group)
+    ranges, send, recv = merge_exchange_plan(counts, strides, slens, N, world, rank)
+    f0, f1 = chunk_bounds(N, world)[rank]
+    sums = torch.empty((sum(b - a for a, b in ranges), HW), dtype=torch.float64, device=shift.device)
+    o = 0
+    for a, b in ranges:
+        K.aligner_merge_partial_window([r if r.shape[0] else None for r in rows], k0, counts, scales, trans,
+                                       strides, slens, a, b - a, HW, shift, x_f32, out=sums[o:o + b - a])
+        o += b - a
+    rbuf = exchange_window_rows(sums, send, [sum(m for _, m in pc) for pc in recv], group)
+    pieces = [pc for src in recv for pc in src]
+    return K.aligner_merge_finish_pieces(rbuf, pieces, counts, strides, slens, f0, f1 - f0, HW)
+
+
+def exchange_window_rows(sums: torch.Tensor, send: Sequence[int], recv: Sequence[int], group) -> torch.Tensor:
+    """The windowed merge's all-to-all: `sums` [rows, ...] (this rank's covered frames in frame order,
+    send[r] rows for rank r, back to back) → the received rows [Σ recv, ...], recv[s] rows from rank s,
+    in source-rank order."""
+    row = math.prod(sums.shape[1:])
+    in_split = [n * row for n in send]
+    out_split = [n * row for n in recv]
+    rbuf = torch.empty((sum(recv), *sums.shape[1:]), dtype=sums.dtype, device=sums.device)
+    if isinstance(group, SliceGroup):  # local no-op: this rank's own rows stand in for every source
+        if rbuf.numel():
+            src = sums.reshape(-1)
+            if src.numel():
+                reps = (rbuf.numel() + src.numel() - 1) // src.numel()
+                rbuf.view(-1).copy_(src.repeat(reps)[:rbuf.numel()])
+            else:
+                rbuf.zero_()
+    elif _via_host(group, sums):
+        h = torch.empty(rbuf.shape, dtype=rbuf.dtype)
+        dist.all_to_all_single(h.view(-1), sums.reshape(-1).cpu(), out_split, in_split, group=group)
+        rbuf.copy_(h)
+    else:
+        dist.all_to_all_single(rbuf.view(-1), sums.reshape(-1), out_split, in_split, group=group)
+    return rbuf
+
+
+def _mark(timing: Optional[list], name: str):
+    """Phase boundary for bench.py's per-phase times: a timing event on the current stream."""
+    if timing is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        timing.append((name, ev))
+
+
 class ShardedOutput:
     """Distributed RollingDepthOutput: this rank's frame chunk [f0, f1) of depth_pred /
     depth_coaligned / input_rgb, its own decoded snippets (snippet_rows[d] are global snippets
@@ -186,7 +305,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
                     to_host: bool = False, refine_step: int = 0, refine_snippet_len: int = 3,
                     refine_start_dilation: int = 6, gather: bool = False, record: Optional[dict] = None,
                     generator: Optional[torch.Generator] = None,
-                    init_infer_steps: Union[int, Sequence[int]] = 1) -> ShardedOutput:
+                    init_infer_steps: Union[int, Sequence[int]] = 1, timing: Optional[list] = None) -> ShardedOutput:
     """Multi-GPU RollingDepthPipeline.forward (every preset: refine_step > 0 included).
 
     `input_frames` is either the whole video [1,N,3,H,W] / [N,3,H,W], or — with `num_frames=N` —
@@ -198,14 +317,15 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     build's own entry point).  `snippet_len`: one length, or one per dilation.  `group` defaults to
     the world group (refine's all-reduce included).  `init_infer_steps`: DDIM steps per snippet, one
     count or one per dilation (rollingdepth_pipeline.py:421-445), as forward().  Without `init_noise` the shared noise is drawn
-    on rank 0 exactly as forward() draws it (from `generator`) and broadcast."""
+    on rank 0 exactly as forward() draws it (from `generator`) and broadcast.  `timing` (a list):
+    phase-boundary events (name, torch.cuda.Event) are appended to it (bench.py --slice-world)."""
     from . import kernels as K
     from .aligner import DepthAligner, check_row_layout
 
     if group is None:
         group = dist.group.WORLD
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    world = _world(group)
+    rank = _rank(group)
     dev = pipe.device
     frames = input_frames[0] if input_frames.dim() == 5 else input_frames
     N = frames.shape[0] if num_frames is None else num_frames
@@ -230,6 +350,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
         raise ValueError(f"rank {rank} holds {mine_frames.shape[0]} frames, expected {f1 - f0}")
     H_in, W_in = frames.shape[-2:]
     h, w = pipe.vae.latent_hw(H_in, W_in)
+    _mark(timing, "start")
     # 1. encode my frame chunk, all-gather the latents
     if f1 > f0:
         mine = pipe.encode_rgb(mine_frames.to(dev))
@@ -243,6 +364,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
             init_noise = torch.empty((1, 4, h, w), device=dev, dtype=pipe.dtype)
         _broadcast(init_noise, 0, group)
     noise = pipe._noise_nhwc(init_noise, h, w)
+    _mark(timing, "encode")
     # 2. my snippets (compact: row r of dilation d is global snippet subsets[d][r])
     counts = [len(pipe.get_snippet_indice(0, [0], N, sl, d, d, 1)) for d, sl in zip(dil, slens)]
     subsets = rank_subsets(counts, world, rank)
@@ -254,6 +376,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     H, W = rows[0].shape[-2:]
     d2h = torch.cuda.Stream(dev) if to_host else None
     snip_host = [pipe._to_host_async(r.to(pipe.dtype), d2h) if r.shape[0] else None for r in rows] if to_host else None
+    _mark(timing, "snippets")
     # 3. co-alignment
     local_mm = [K.minmax(r) for r in rows if r.shape[0]]
     mm = K.minmax(torch.stack(local_mm).reshape(-1)) if local_mm else \
@@ -267,12 +390,12 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
     strides = list(dil)
     seq_len = aligner.sequence_length(counts, slens[0], dil)
     assert seq_len == N
+    _mark(timing, "prepare")
     scales, trans, hist, ws = aligner.optimize_prepared(xs, strides, N)
     rows_f32 = rows[0].dtype == F32
-    sums = K.aligner_merge_partial([r if r.shape[0] else None for r in rows], k0, counts, scales, trans, strides,
-                                   slens, N, H * W, shift, x_f32=1 if rows_f32 else (2 if pipe.merge_f32 else 0))
-    my_sums = _reduce_scatter_rows(sums, world, group)
-    merged = K.aligner_merge_finish(my_sums, counts, strides, slens, f0) if f1 > f0 else my_sums.float()
+    _mark(timing, "aligner")
+    merged = _merge_windowed(rows, k0, counts, scales, trans, strides, slens, N, H * W, shift,
+                             1 if rows_f32 else (2 if pipe.merge_f32 else 0), group)
     # merge_scaled_triplets returns the snippets' dtype (unless the pipeline merges in f32)
     d = (merged if (pipe.merge_f32 or rows_f32) else merged.to(pipe.dtype).float()).contiguous()
     mm_d = K.minmax(d) if d.numel() else torch.tensor([float("inf"), float("-inf")], device=dev)
@@ -281,6 +404,7 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
         K.renormalize_(d, gmm)
     coaligned = d.to(pipe.dtype).view(f1 - f0, 1, H, W)
     del ws
+    _mark(timing, "merge")
     # 4. refine
     if refine_step > 0:
         if f1 > f0:
@@ -300,6 +424,8 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
         depth = depth.view(f1 - f0, 1, H, W).to(pipe.dtype)
     else:
         depth = coaligned
+    if refine_step > 0:
+        _mark(timing, "refine")
     if record is not None:
         record.update(rgb_latent=rgb_latent, scales=scales, translations=trans, dilations=list(dil),
                       loss_history=hist)
@@ -314,4 +440,5 @@ def sharded_forward(pipe, input_frames: torch.Tensor, dilations: List[int], cap_
         if f1 > f0:
             out.input_rgb = pipe._to_host_async(mine_frames.to(dev, pipe.dtype) / 2.0 + 0.5, d2h)
         d2h.synchronize()
+    _mark(timing, "egress")
     return out

@@ -101,6 +101,54 @@ def test_aligner_merge_f16_rounding():
     assert np.abs(got - ref[:, 0].astype(np.float32)).max() <= 2e-3
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("f32", [False, True])
+def test_aligner_merge_windowed_bitwise(world, f32):
+    """The sharded merge over frame windows (round 5: rdmi_aligner_merge_partial_window per rank, the
+    all-to-all of shard.merge_exchange_plan done here by slicing, rdmi_aligner_merge_finish_pieces)
+    equals the single-GPU rdmi_aligner_merge bitwise (f64 sums), for W ranks emulated in one process —
+    including ranks that own no snippet (W = 8 > snippets of some dilations) and mixed lengths."""
+    from rollingdepth_amd import kernels as K
+    from rollingdepth_amd.shard import chunk_bounds, merge_exchange_plan, rank_subsets
+
+    N = 23
+    snips, dil = _synth(N=N, dil=(1, 4, 7), H=24, W=20, seed=3, lengths=[3, 2, 2],
+                        dtype=np.float32 if f32 else np.float16)
+    rng = np.random.default_rng(4)
+    xf = [torch.from_numpy(x[:, :, 0]).to(DEV) for x in snips]
+    n = [x.shape[0] for x in xf]
+    w = [x.shape[1] for x in xf]
+    sc = [torch.from_numpy((1 + 0.1 * rng.standard_normal(m)).astype(np.float32)).to(DEV) for m in n]
+    tr = [torch.from_numpy((0.1 * rng.standard_normal(m)).astype(np.float32)).to(DEV) for m in n]
+    shift = torch.tensor([min(float(x.min()) for x in xf)], dtype=torch.float32, device=DEV)
+    HW = 24 * 20
+    ref = K.aligner_merge(xf, sc, tr, dil, N, shift, f32_arith=True).reshape(N, HW)
+    mode = 1 if f32 else 2
+    sent = []
+    for r in range(world):
+        sub = rank_subsets(n, world, r)
+        k0 = [x[0] if x else 0 for x in sub]
+        rows = [xf[d][k0[d]:k0[d] + len(sub[d])] for d in range(len(n))]
+        ranges, send, _ = merge_exchange_plan(n, dil, w, N, world, r)
+        sums = torch.cat([K.aligner_merge_partial_window([x if x.shape[0] else None for x in rows], k0, n, sc, tr,
+                                                         dil, w, a, b - a, HW, shift, mode) for a, b in ranges]) \
+            if ranges else torch.zeros((0, HW), dtype=torch.float64, device=DEV)
+        assert sums.shape[0] == sum(send)
+        o, per_dst = 0, []
+        for m in send:
+            per_dst.append(sums[o:o + m])
+            o += m
+        sent.append(per_dst)
+    got = []
+    for r in range(world):
+        f0, f1 = chunk_bounds(N, world)[r]
+        _, _, recv = merge_exchange_plan(n, dil, w, N, world, r)
+        rbuf = torch.cat([sent[s][r] for s in range(world)])
+        pieces = [pc for src in recv for pc in src]
+        got.append(K.aligner_merge_finish_pieces(rbuf.contiguous(), pieces, n, dil, w, f0, f1 - f0, HW))
+    assert torch.equal(torch.cat(got), ref)
+
+
 @pytest.mark.parametrize("case", ["small", "mixed", "metric"])
 def test_aligner_fused_loop_bitwise(case, monkeypatch):
     """The two-launch iteration (aligner.hip snippet_grad_adam: per-snippet last-chunk Adam, deferred

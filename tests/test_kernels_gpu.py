@@ -81,7 +81,9 @@ def test_gemm_geglu(engine):
     w = torch.randn(8 * C, C, device=DEV, generator=g) / math.sqrt(C)
     b = torch.randn(8 * C, device=DEV, generator=g) * 0.1
     wp, bp = K_.geglu_permute(w.cpu(), b.cpu())
-    y = K_.gemm(a, K_.pack_linear(wp, DEV), C, bias=bp.to(DEV), geglu=True)
+    # NaN-filled output: an epilogue that leaves elements unwritten fails here
+    y = torch.full((M, 4 * C), float("nan"), dtype=torch.float16, device=DEV)
+    K_.gemm(a, K_.pack_linear(wp, DEV), C, out=y, bias=bp.to(DEV), geglu=True)
     h, gate = (a.float() @ w.half().float().t() + b).chunk(2, dim=-1)
     ref = h * F.gelu(gate)
     assert y.shape == (M, 4 * C)

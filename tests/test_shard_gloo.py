@@ -55,7 +55,8 @@ def _worker(rank, world, port, res):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import rd_oracle as O
     from rollingdepth_amd.shard import (_all_gather_rows, _all_reduce_minmax, _broadcast, _reduce_scatter_rows,
-                                        chunk_bounds, gather_rows_by_dilation, rank_subsets)
+                                        chunk_bounds, exchange_window_rows, frame_ranges, gather_rows_by_dilation,
+                                        merge_exchange_plan, rank_subsets)
 
     ok = True
     # --- flat split + all-gather of per-snippet rows (the aligner inputs) -----------------------
@@ -108,6 +109,28 @@ def _worker(rank, world, port, res):
                           [t.numpy() for t in tr], N)
     err = np.abs(merged.numpy() - ref.reshape(N, H * W)).max()
     ok &= bool(err < 1e-5)
+    # --- windowed merge (round 5): sums over the rank's covered frame ranges only, all-to-all of the rows
+    # each chunk needs, pieces added per frame in source-rank order (rdmi_aligner_merge_finish_pieces) --
+    ranges, send, recv = merge_exchange_plan(n, dil, w, N, world, rank)
+    ok &= ranges == frame_ranges(sub, dil, w)
+    covered = {f for d in range(len(dil)) for k in sub[d] for j in range(w[d]) for f in [k + j * dil[d]]}
+    inr = {f for a, b in ranges for f in range(a, b)}
+    ok &= covered <= inr and all(b1 < a2 for (_, b1), (a2, _) in zip(ranges, ranges[1:]))
+    wsum = torch.cat([sums[a:b] for a, b in ranges]).double() if ranges else torch.zeros((0, H * W),
+                                                                                          dtype=torch.float64)
+    ok &= sum(send) == wsum.shape[0]
+    rbuf = exchange_window_rows(wsum, send, [sum(m for _, m in pc) for pc in recv], None)
+    acc = torch.zeros((f1 - f0, H * W), dtype=torch.float64)
+    o = 0
+    for src in recv:
+        for a, m in src:
+            acc[a - f0:a - f0 + m] += rbuf[o:o + m]
+            o += m
+    ok &= o == rbuf.shape[0]
+    mine_w = torch.stack([acc[i] / _cover(n, dil, w, f0 + i) for i in range(f1 - f0)]).float() if f1 > f0 \
+        else torch.zeros((0, H * W))
+    merged_w = _all_gather_rows(mine_w, N, world)
+    ok &= bool(np.abs(merged_w.numpy() - ref.reshape(N, H * W)).max() < 1e-5)
     # --- refine step: rank-local sums of its snippets' predictions, all-reduce, ÷ cover count ---------
     Nf, L, P, C = 13, 3, 6, 4
     stride = 2
