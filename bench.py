@@ -470,7 +470,7 @@ def main():
             "value": round(total_frames / dt, 4), "unit": "depth frames/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 1), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "data": "synthetic",
-            "dtype": pr["dtype"] + (" (bf16x3 products)" if pr["dtype"] == "f32" and K.f32_x3() else ""),
+            "dtype": pr["dtype"] + (f" ({K.f32_precision_label()})" if pr["dtype"] == "f32" else ""),
             "config": {"workload": f"{a.preset} preset: {N}-frame {res}x{res} video, dilations {dil0} "
                                    f"(cap_dilation={pr['cap']}), snippet_len 3, 1-step DDIM, aligner "
                                    f"{a.aligner_iters} it, refine {refine}; SD2-shaped UNet+VAE random-init",

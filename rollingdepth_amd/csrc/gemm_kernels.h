@@ -1789,29 +1789,29 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   unsigned inmask = 0;  // bit e: this lane's pixel of halo piece e lies inside the image
 #pragma unroll
   for (int e = 0; e < HPW; ++e) inmask |= (hoff[e] != OOB ? 1u : 0u) << e;
+  // in-place GroupNorm (+SiLU) of this wave's landed pieces: the instructions of
+  // conv_halo_occ2_kernel's transform (gn_xform_words: v_fma_mix affine, silu4, packed RNE
+  // conversion, padding only in waves holding out-of-image pixels) — bitwise the unfused
+  // gn_apply; the lane's logical chunk (and so its 8 scale / shift values) changes per piece here
   auto xformHalo = [&](int cb) {
-    const int npc = (HPC - wids + 3) / 4;  // pieces of this wave
-#pragma unroll 1
-    for (int e = 0; e < npc; ++e) {
-      {
+#pragma unroll
+    for (int e = 0; e < HPW; ++e)
+      if (hv(e)) {
         f16* lh = lds + (wid + 4 * e) * 8 * BKP + lane * 8;
         const float* ts = gnt + cb * 64 + hlc(e) * 8;
         const f32x4 s0 = *(const f32x4*)ts, s1 = *(const f32x4*)(ts + 4);
         const f32x4 h0 = *(const f32x4*)(ts + GNT), h1 = *(const f32x4*)(ts + GNT + 4);
         const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
         const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
-        const f16x8 v = *(const f16x8*)lh;
+        unsigned w[4];
+        *(f16x8*)w = *(const f16x8*)lh;
         const bool in = (inmask >> e) & 1;
-        f16x8 o;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float f = fmaf((float)v[i], sc[i], sh[i]);
-          if (p.gsilu) f = silu_f(f);
-          o[i] = in ? (f16)f : (f16)0.f;
-        }
-        *(f16x8*)lh = o;
+        if (p.gsilu)
+          gn_xform_words<4, true>(w, sc, sh, in);
+        else
+          gn_xform_words<4, false>(w, sc, sh, in);
+        *(f16x8*)lh = *(const f16x8*)w;
       }
-    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
@@ -1932,6 +1932,67 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   // The optional parts are wave-uniform: one instantiation per (residual, SiLU) so that neither is
   // if-converted into every output.
   const long rbg = p.rowbias ? (long)b * p.rb_ld : 0;  // conv row bias: one group per image
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned;
+  // Specialised epilogue (no SiLU), as store_fast: the residual's f16 halves and the moments' f16
+  // outputs enter the f32 sums through v_fma_mix_f32, the moment row sums are DPP adds (the same
+  // operations in the same order as the generic form below: bitwise its outputs and moments).
+  auto epi_fast = [&](auto RESc, auto MOMc) {
+    constexpr bool RES = decltype(RESc)::value, MOM = decltype(MOMc)::value;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int nb = n0 + 64 * wn + 32 * c + 16 * hh;
+      f32x4 badd[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        badd[q] = p.bias ? *(const f32x4*)(p.bias + nb + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (p.rowbias) badd[q] += *(const f32x4*)(p.rowbias + rbg + nb + 4 * q);
+      }
+      const long m0 = (long)(b * p.Ho + y0 + 4 * wm) * p.Wo + x0 + j;
+      u32x4 rr[4][2];
+      if constexpr (RES) {
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          const f16* rrow = p.R + (m0 + (long)pb * p.Wo) * p.ldr + nb;
+          rr[pb][0] = *(const u32x4*)rrow;
+          rr[pb][1] = *(const u32x4*)(rrow + 8);
+        }
+      }
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        unsigned ow[8];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          float v0 = fmaf(acc[pb][c][2 * h], p.alpha, badd[h >> 1][(2 * h) & 3]);
+          float v1 = fmaf(acc[pb][c][2 * h + 1], p.alpha, badd[h >> 1][(2 * h + 1) & 3]);
+          if constexpr (RES) {
+            v0 = add_h<false>(v0, rr[pb][h >> 2][h & 3]);
+            v1 = add_h<true>(v1, rr[pb][h >> 2][h & 3]);
+          }
+          asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(ow[h]) : "v"(v0), "v"(v1));
+        }
+        f16* crow = (f16*)p.C + (m0 + (long)pb * p.Wo) * p.ldc + nb;
+        *(u32x4*)crow = u32x4{ow[0], ow[1], ow[2], ow[3]};
+        *(u32x4*)(crow + 8) = u32x4{ow[4], ow[5], ow[6], ow[7]};
+        if constexpr (MOM) {  // slot (4-channel group, the 32 pixels of this fragment row)
+          const long slot = ((long)(b * p.Ho + y0 + 4 * wm + pb) * p.Wo + x0) >> 5;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float s = add_h<true>(add_h<false>(0.f, ow[2 * g]), ow[2 * g]);
+            s = add_h<true>(add_h<false>(s, ow[2 * g + 1]), ow[2 * g + 1]);
+            float q = sq_h<true>(sq_h<false>(0.f, ow[2 * g]), ow[2 * g]);
+            q = sq_h<true>(sq_h<false>(q, ow[2 * g + 1]), ow[2 * g + 1]);
+            row16_sum2(s, q);
+            s += dpp_f<0x142>(s);  // row_bcast:15 — rows 1 and 3 add the sums of rows 0 and 2
+            q += dpp_f<0x142>(q);
+            if ((lane & 31) == 16) {
+              float* d = p.gnp + (long)((nb + 4 * g) >> 2) * p.gn_ld + slot * 2;
+              *(__attribute__((ext_vector_type(2))) float*)d = {s, q};
+            }
+          }
+        }
+      }
+    }
+  };
   auto epilogue = [&](auto RESc, auto SILUc) {
     constexpr bool RES = decltype(RESc)::value, SILU = decltype(SILUc)::value;
 #pragma unroll
@@ -1996,10 +2057,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (p.R) {
-    if (p.silu) epilogue(T_{}, T_{}); else epilogue(T_{}, F_{});
+  if (p.silu) {
+    if (p.R) epilogue(T_{}, T_{}); else epilogue(F_{}, T_{});
+  } else if (p.R) {
+    if (p.gnp) epi_fast(T_{}, T_{}); else epi_fast(T_{}, F_{});
   } else {
-    if (p.silu) epilogue(F_{}, T_{}); else epilogue(F_{}, F_{});
+    if (p.gnp) epi_fast(F_{}, T_{}); else epi_fast(F_{}, F_{});
   }
 }
 

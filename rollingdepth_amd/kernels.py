@@ -93,15 +93,34 @@ def _need_act(t: torch.Tensor, name: str):
 BF16 = torch.bfloat16
 
 
-def f32_x3() -> bool:
-    """Whether f32 weights are packed for the bf16-split engine (RDMI_F32_X3, rdmi.h; the default;
-    read when the weights are packed, and by attention() at each call for its own products):
-    f32 activations and accumulation, three bf16 MFMA products per multiply-add (≈2^-16 relative per
-    product, 2.2× the exact engine's speed on the paper preset's shapes: profiles/r03f_x3_probe.log).
-    The reference's fp32 preset runs its convolutions through cuDNN with PyTorch's default
-    allow_tf32 (run_video.py sets no precision flag), i.e. with 2^-11 products on its Ampere+ GPUs.
-    RDMI_F32_X3=0 keeps exact f32 products (v_mfma_f32_16x16x4_f32).  Read at pack time."""
-    return os.environ.get("RDMI_F32_X3", "1") == "1"
+def _f32_x3_mode() -> str:
+    m = os.environ.get("RDMI_F32_X3", "conv")
+    if m not in ("0", "1", "conv"):
+        raise ValueError(f"RDMI_F32_X3={m!r}: 0 (exact f32 products everywhere), conv (default: bf16-split "
+                         f"products in the convolutions only) or 1 (bf16-split products everywhere)")
+    return m
+
+
+def f32_x3(kind: str = "conv") -> bool:
+    """Whether the f32 path runs `kind` ("conv" | "linear" — Linear layers and the cross-frame
+    attention) on the bf16-split engine (RDMI_F32_X3, rdmi.h): f32 activations and accumulation,
+    three bf16 MFMA products per multiply-add (≈2^-16 relative per product, 2.2× the exact engine's
+    speed on the paper preset's shapes: profiles/r03f_x3_probe.log).  Read when the weights are packed,
+    and by attention() at each call for its own products.
+    The default (RDMI_F32_X3=conv, round 5) follows the reference's fp32 preset precision layer by
+    layer: its convolutions run through cuDNN under PyTorch's default allow_tf32 (run_video.py sets no
+    precision flag), 2^-11 products on its Ampere+ GPUs — bf16x3 (2^-16) is finer — while its Linear
+    layers (matmul: allow_tf32 off by default) and SDPA are exact f32, and so are ours (the exact-f32
+    engines, v_mfma_f32_16x16x4_f32).  RDMI_F32_X3=1: bf16x3 everywhere (the round-3/4 default, a
+    labelled faster variant); RDMI_F32_X3=0: exact f32 products everywhere."""
+    m = _f32_x3_mode()
+    return m == "1" or (m == "conv" and kind == "conv")
+
+
+def f32_precision_label() -> str:
+    """The f32 path's product precision, for bench lines."""
+    return {"0": "exact f32 products", "conv": "bf16x3 conv products, exact f32 Linear/attention",
+            "1": "bf16x3 products"}[_f32_x3_mode()]
 
 
 def split_bf16(w: torch.Tensor) -> torch.Tensor:
@@ -122,7 +141,7 @@ def pack_linear(w: torch.Tensor, device, dtype=F16) -> torch.Tensor:
     kp = (k + 31) // 32 * 32
     out = torch.zeros((n, kp), dtype=dtype, device=device)
     out[:, :k] = w.to(device=device, dtype=dtype)
-    return split_bf16(out) if dtype == F32 and f32_x3() else out
+    return split_bf16(out) if dtype == F32 and f32_x3("linear") else out
 
 
 def _w_code(a: torch.Tensor, w: torch.Tensor, name: str) -> int:
@@ -168,7 +187,7 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16)
     kp = (k + 31) // 32 * 32
     out = torch.zeros((co, kp), dtype=dtype)
     out[:, :k] = t.reshape(co, k).to(dtype)
-    if dtype == F32 and f32_x3():
+    if dtype == F32 and f32_x3("conv"):
         out = split_bf16(out)
     return out.to(device)
 
@@ -543,7 +562,7 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
         out = torch.empty((B, Sq, HD), dtype=q.dtype, device=q.device)
     sc = 1.0 / math.sqrt(D) if scale is None else scale
     code = _dtype_code(q)
-    if code == _N.RDMI_F32 and f32_x3():
+    if code == _N.RDMI_F32 and f32_x3("linear"):
         code = _N.RDMI_F32_X3  # bf16-split products (attention_f32.hip attn_fwd_f32x3)
     name = {_N.RDMI_F16: "attention_fwd", _N.RDMI_F32: "attention_fwd_f32", _N.RDMI_F32_X3: "attention_fwd_f32x3"}[code]
     es = q.element_size()

@@ -341,22 +341,42 @@ class RollingDepthPipeline:
         """rollingdepth_pipeline.py:356-463 with snippets batched per UNet call.
         rgb_latent NHWC [N,h,w,8]; init_noise NHWC [1,h,w,8].  Returns per dilation the decoded
         snippets [n_d, w, H, W] in depth_dtype (device).  `snippet_subset[d]` (optional) restricts the work
-        to those snippet indices (multi-GPU sharding); other rows are left uninitialised."""
+        to those snippet indices (multi-GPU sharding); other rows are left uninitialised.  With a
+        subset, the snippets of consecutive dilations that share a snippet length and a DDIM step count
+        run in the same UNet batches and decode chunks (a rank of an 8-way split holding 3 snippets of
+        one dilation and 16 of the next runs one 19-snippet batch, not 3 + 16: bench.py --slice-world,
+        DESIGN.md §5); the per-dilation outputs are then consecutive views of one buffer."""
         self._context()
         N, h, w, _ = rgb_latent.shape
         H, W = h * self.vae.factor, w * self.vae.factor
-        outs = []
+        jobs = []  # (dilation index, snippet list, frame indices per snippet)
         for di, (dil, slen, stride, steps) in enumerate(zip(dilations, snippet_lengths, strides, init_infer_steps)):
             self.scheduler.set_timesteps(steps)
-            timesteps = self.scheduler.timesteps
-            idx = self.get_snippet_indice(0, timesteps, N, slen, dil, dil, stride)
+            idx = self.get_snippet_indice(0, self.scheduler.timesteps, N, slen, dil, dil, stride)
             todo = list(range(len(idx))) if snippet_subset is None else list(snippet_subset[di])
-            # row r of the output is snippet todo[r] (all snippets unless a subset is given)
-            buf = torch.empty((len(todo), slen, H, W), dtype=self.depth_dtype, device=self.device)
-            fidx_all = self._device_index([f for s in todo for f in idx[s]]) if todo else None
-            for b0, b1 in self._snippet_batches(len(todo), slen, h, w):
-                sel = todo[b0:b1]
-                fidx = fidx_all[b0 * slen:(b0 + len(sel)) * slen]
+            jobs.append((di, todo, [idx[k] for k in todo]))
+        groups = []  # runs of dilations batched together
+        for di, todo, fr in jobs:
+            key = (snippet_lengths[di], init_infer_steps[di])
+            if snippet_subset is not None and groups and groups[-1][0] == key:
+                groups[-1][1].append((di, todo, fr))
+            else:
+                groups.append((key, [(di, todo, fr)]))
+        outs: List[Optional[torch.Tensor]] = [None] * len(dilations)
+        for (slen, steps), members in groups:
+            self.scheduler.set_timesteps(steps)
+            timesteps = self.scheduler.timesteps
+            ntodo = sum(len(t) for _, t, _ in members)
+            # row r of the group buffer is the r-th snippet of the members' todo lists, in order
+            buf = torch.empty((ntodo, slen, H, W), dtype=self.depth_dtype, device=self.device)
+            o = 0
+            for di, todo, _ in members:
+                outs[di] = buf[o:o + len(todo)]
+                o += len(todo)
+            fidx_all = self._device_index([f for _, _, fr in members for s in fr for f in s]) if ntodo else None
+            for b0, b1 in self._snippet_batches(ntodo, slen, h, w):
+                nb = b1 - b0
+                fidx = fidx_all[b0 * slen:b1 * slen]
                 x = K.gather_unet_input(rgb_latent, init_noise, fidx, depth_bcast=True)
                 depth_view = x[..., 4:8]
                 for si, t in enumerate(timesteps.tolist()):
@@ -379,9 +399,8 @@ class RollingDepthPipeline:
                         self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4, out=x2[..., 4:])
                         x = x2
                         depth_view = x[..., 4:8]
-                self.decode_depth(zin, buf[b0:b1].view(len(sel) * slen, H, W, 1))
-                _progress(f"dilation {dil}: snippets {b1}/{len(todo)} decoded")
-            outs.append(buf)
+                self.decode_depth(zin, buf[b0:b1].view(nb * slen, H, W, 1))
+                _progress(f"dilations {[dilations[m[0]] for m in members]}: snippets {b1}/{ntodo} decoded")
         return outs
 
     def refine(self, rgb_latent: torch.Tensor, depth_latents: torch.Tensor, init_noise: torch.Tensor,
