@@ -124,6 +124,13 @@ typedef struct rdmi_conv_args {
    * 256-channel halo engine runs the conv (f16, Cout % 256 == 0, Cin % 64 == 0, Ho % 32 == 0,
    * Wo % 32 == 0, no input GroupNorm); elsewhere `w` is used.  NULL: off. */
   const void* w_up2;
+  /* Optional with in_mean_rstd (round 5): the input GroupNorm's per-channel scale / shift as
+   * rdmi_groupnorm_affine writes them, [B][Cin/64][2][64] f32 — per image and 64-channel block the 64
+   * scales sc = rstd·gamma[c], then the 64 shifts sh = beta[c] − mean·sc.  With it the
+   * two-workgroups-per-CU halo engine fuses the norm for any Cin % 64 == 0 (each wave loads the block's
+   * 8 + 8 values of its lanes with the halo refill); without it only for Cin ≤ 256 (the table built in
+   * LDS).  The values are the ones the kernel would compute itself: bitwise the same results. */
+  const float* in_affine;
 } rdmi_conv_args;
 int rdmi_conv2d(const rdmi_conv_args* args, void* stream);
 /* 1 if rdmi_conv2d fuses an input GroupNorm for this shape (in_groups set; pointers not read) */
@@ -144,6 +151,11 @@ int rdmi_groupnorm_stats(const void* x, int dtype, int B, long HW, int C, int G,
  * group's partials in a fixed order — independent of how many images share the tensor. */
 int rdmi_groupnorm_stats_partials(const float* part, long part_ld, int B, long HW, int C, int G, float eps,
                                   float* mean_rstd, void* stream);
+/* Input-GroupNorm scale / shift table for rdmi_conv_args.in_affine: out [B][C/64][2][64] f32, per image b
+ * and 64-channel block the scales rstd·gamma[c] then the shifts beta[c] − mean·(rstd·gamma[c]) — the f32
+ * arithmetic of rdmi_groupnorm_apply (mean_rstd as rdmi_groupnorm_stats writes it; C % 64 == 0). */
+int rdmi_groupnorm_affine(const float* mean_rstd, const float* gamma, const float* beta, int B, int C, int G,
+                          float* out, void* stream);
 int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, long HW, int C, int G,
                          const float* mean_rstd, const float* gamma, const float* beta, int silu,
                          void* stream);

@@ -45,6 +45,7 @@ class ConvArgs(C.Structure):
         ("in_mean_rstd", vp), ("in_gamma", vp), ("in_beta", vp), ("in_groups", i32), ("in_silu", i32),
         ("dtype", i32),
         ("w_up2", vp),
+        ("in_affine", vp),
     ]
 
 
@@ -106,6 +107,7 @@ _SIGS = {
                                          vp, vp, vp]),
     "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64, vp, vp,
                                         vp]),
+    "rdmi_groupnorm_affine": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
     "rdmi_aligner_merge_partial_window": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp),
                                                 C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
                                                 C.POINTER(i32), i32, i32, i64, vp, vp, vp]),

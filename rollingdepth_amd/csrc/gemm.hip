@@ -152,10 +152,11 @@ bool halo_eligible(const rdmi_conv_args* a, int hmode) {
          a->Ho == (a->upsample ? 2 * a->H : a->H) && a->Wo == (a->upsample ? 2 * a->W : a->W);
 }
 
-// input GroupNorm: groups divide Cin, the LDS scale/shift table holds ≤ 1024 channels (≤ 256 in
-// the two-workgroups-per-CU variant, the only one for Cout % 256 != 0 other than 128)
+// input GroupNorm: groups divide Cin; without in_affine the LDS scale/shift table holds ≤ 1024
+// channels (≤ 256 in the two-workgroups-per-CU variant, the only one for Cout % 256 != 0 other than
+// 128); with in_affine (the table in global memory, read per channel block) any Cin
 bool in_gn_ok(const rdmi_conv_args* a) {
-  const int cmax = (a->Cout % 256 == 0 || a->Cout == 128) ? 1024 : 256;
+  const int cmax = a->in_affine ? (1 << 30) : (a->Cout % 256 == 0 || a->Cout == 128) ? 1024 : 256;
   return a->in_groups > 0 && a->Cin <= cmax && a->Cin % a->in_groups == 0;
 }
 
@@ -262,6 +263,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     p.cperm = (!cp || cp[0] != '0') && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 &&
               (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0));
     p.gmr = a->in_mean_rstd; p.ggam = a->in_gamma; p.gbet = a->in_beta; p.gG = a->in_groups; p.gsilu = a->in_silu;
+    p.gaff = a->in_mean_rstd ? a->in_affine : nullptr;
+    RDMI_REQUIRE(!p.gaff || ((uintptr_t)p.gaff & 15) == 0, RDMI_E_ALIGN, "conv2d: in_affine not 16-byte aligned");
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
     const bool gn = p.gmr != nullptr;
@@ -270,7 +273,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
       p.Wt = (const f16*)a->w_up2; p.ldw = 4L * a->Cin; p.K = p.Kvalid = 4 * a->Cin;
       p.w_bytes = (unsigned)(4L * a->Cout * p.ldw * 2);
       launch_conv_halo(3, 2, 4, false, dim3(a->Cout / 256, patches, 1), st, p);
-    } else if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256))) {
+    } else if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256 || p.gaff))) {
       dim3 g(a->Cout / 256, patches, 1);
       const bool ph2 = hmode != 1 || gn;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
       if (a->upsample) {
@@ -278,7 +281,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
       } else {
         launch_conv_halo(1, ph2 ? 2 : 4, 4, ph2 && gn, g, st, p);
       }
-    } else if (a->Cout == 128 && (hmode == 4 || (gn && a->Cin > 256))) {  // the 8-wave 128-channel variant
+    } else if (a->Cout == 128 && (hmode == 4 || (gn && a->Cin > 256 && !p.gaff))) {  // the 8-wave 128-channel variant
       dim3 g(1, patches, 1);
       launch_conv_halo(a->upsample ? 2 : 1, 1, 2, gn, g, st, p);
     } else if (h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches

@@ -35,6 +35,7 @@ struct GemmP {
   int group_m;  // tile order inside an XCD's range: groups of group_m m-tiles, n-tiles within a group
   // GroupNorm (+SiLU) of the conv INPUT, applied as it is read (conv_halo_kernel<..., GN = true>)
   const float* gmr; const float* ggam; const float* gbet; int gG, gsilu;
+  const float* gaff;  // optional [B][Cin/64][2][64] scale / shift table (rdmi_conv_args.in_affine)
   int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
   int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
   unsigned long long* stamps;  // STAMP builds only (tools/conv_stamp.hip): per-wave segment cycle sums
@@ -1514,13 +1515,30 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
 #pragma unroll
     for (int e = 0; e < NB; ++e) dma16s(rw_, bvo[e], u * BKP * 2, lb + (wids + 4 * e) * 8 * BKP);
   };
+  // The lane's 8 scales / shifts of channel block cb: from the global table p.gaff (any Cin; the four
+  // 16-B loads issued with the halo DMA, so the refill's vmcnt wait covers them), else from the LDS
+  // table the prologue built (Cin ≤ 256).  Same values either way.
+  f32x4 aff[4];
+  auto loadAff = [&](int cb) {
+    if (p.gaff) {
+      const float* ta = p.gaff + ((long)b * ncb + cb) * 128 + chunk * 8;
+      aff[0] = *(const f32x4*)ta;
+      aff[1] = *(const f32x4*)(ta + 4);
+      aff[2] = *(const f32x4*)(ta + 64);
+      aff[3] = *(const f32x4*)(ta + 68);
+    }
+  };
   // in-place GroupNorm (+SiLU) of this wave's landed pieces of the halo of channel block cb
   auto xformHalo = [&](int cb) {
-    const float* ts = gnt + cb * 64 + chunk * 8;
-    const f32x4 s0 = *(const f32x4*)ts, s1 = *(const f32x4*)(ts + 4);
-    const f32x4 h0 = *(const f32x4*)(ts + GNT), h1 = *(const f32x4*)(ts + GNT + 4);
-    const float sc[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
-    const float sh[8] = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+    if (!p.gaff) {
+      const float* ts = gnt + cb * 64 + chunk * 8;
+      aff[0] = *(const f32x4*)ts;
+      aff[1] = *(const f32x4*)(ts + 4);
+      aff[2] = *(const f32x4*)(ts + GNT);
+      aff[3] = *(const f32x4*)(ts + GNT + 4);
+    }
+    const float sc[8] = {aff[0][0], aff[0][1], aff[0][2], aff[0][3], aff[1][0], aff[1][1], aff[1][2], aff[1][3]};
+    const float sh[8] = {aff[2][0], aff[2][1], aff[2][2], aff[2][3], aff[3][0], aff[3][1], aff[3][2], aff[3][3]};
 #pragma unroll
     for (int e = 0; e < HPW; ++e)
       if (hv(e)) {
@@ -1551,7 +1569,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   // prologue: halo(0), B(0) [, GroupNorm scale/shift of image b]
   issueHalo(0);
   issueB(0);
-  if constexpr (GN) {
+  if constexpr (GN) loadAff(0);
+  if (GN && !p.gaff) {
     const int c = tid;
     float mean = 0.f, rstd = 0.f, gm = 0.f, bt = 0.f;
     if (c < p.Cin) {
@@ -1588,7 +1607,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
         __builtin_amdgcn_s_barrier();  // every wave is past its reads of halo(cb-1)
         asm volatile("" ::: "memory");
         issueHalo(cb);
-        wait_vmcnt<0>();  // B(u) and the halo pieces of this wave
+        if constexpr (GN) loadAff(cb);
+        wait_vmcnt<0>();  // B(u) and the halo pieces of this wave (and its scale / shift loads)
         if constexpr (GN) xformHalo(cb);
       } else {
         wait_vmcnt<0>();  // B(u), issued one K-tile ago

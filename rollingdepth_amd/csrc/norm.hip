@@ -343,6 +343,41 @@ extern "C" int rdmi_groupnorm_stats_partials(const float* part, long part_ld, in
   return rdmi::check_launch("groupnorm_stats_partials");
 }
 
+namespace {
+
+// Input-GroupNorm table of the fused halo conv (rdmi_conv_args.in_affine): the scale / shift of
+// gn_apply, written per image and 64-channel block as [2][64].
+__global__ __launch_bounds__(256) void gn_affine_k(const float* __restrict__ mr, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, int B, int C, int G,
+                                                   float* __restrict__ out) {
+  const int cpg = C / G;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < (long)B * C; i += (long)gridDim.x * 256) {
+    const int b = (int)(i / C), c = (int)(i - (long)b * C);
+    const int g = c / cpg;
+    const float mean = mr[2 * (b * G + g)], rstd = mr[2 * (b * G + g) + 1];
+    const float sc = rstd * gamma[c];
+    const float sh = beta[c] - mean * sc;
+    float* o = out + ((long)b * (C >> 6) + (c >> 6)) * 128 + (c & 63);
+    o[0] = sc;
+    o[64] = sh;
+  }
+}
+
+}  // namespace
+
+extern "C" int rdmi_groupnorm_affine(const float* mean_rstd, const float* gamma, const float* beta, int B, int C,
+                                     int G, float* out, void* stream) {
+  RDMI_REQUIRE(mean_rstd && gamma && beta && out, RDMI_E_ARG, "groupnorm_affine: null pointer");
+  RDMI_REQUIRE(B > 0 && C > 0 && C % 64 == 0 && G > 0 && C % G == 0, RDMI_E_ARG, "groupnorm_affine: bad B=%d C=%d G=%d",
+               B, C, G);
+  long n = (long)B * C;
+  long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(gn_affine_k, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, mean_rstd, gamma, beta,
+                     B, C, G, out);
+  return rdmi::check_launch("groupnorm_affine");
+}
+
 extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, long HW, int C, int G, const float* mean_rstd,
                                     const float* gamma, const float* beta, int silu, void* stream) {
   RDMI_REQUIRE(x && y && mean_rstd && gamma && beta, RDMI_E_ARG, "groupnorm_apply: null pointer");

@@ -395,6 +395,14 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
                    w_up2)
     a.dtype = code
     a.Kp = kp
+    aff = None
+    if in_gn is not None and not f32 and Cin > 256 and Cin % 64 == 0:
+        # the norm's scale / shift table for the two-workgroups-per-CU halo engine (rdmi.h in_affine)
+        mr, gamma, beta, groups, _ = in_gn
+        aff = torch.empty((B, Cin // 64, 2, 64), dtype=F32, device=x.device)
+        check(lib.rdmi_groupnorm_affine(mr.data_ptr(), gamma.data_ptr(), beta.data_ptr(), B, Cin, groups,
+                                        aff.data_ptr(), _stream()), "rdmi_groupnorm_affine")
+        a.in_affine = aff.data_ptr()
     if part is not None:
         a.gn_part, a.gn_ld = part.data_ptr(), part.stride(0)
     elif _gn_slot is not None:
@@ -444,6 +452,8 @@ def conv2d_in_gn_supported(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, 
     a = _conv_args(x, w, cout, k, stride, pad, None, upsample, None, None, rowbias, None, 1.0, Ho, Wo,
                    (None, None, None, groups, 0))
     a.dtype = _N.RDMI_F32 if x.dtype == F32 else _N.RDMI_F16
+    if x.dtype != F32 and Cin > 256 and Cin % 64 == 0:
+        a.in_affine = 16  # conv2d passes the scale / shift table here (the query reads no pointer)
     return bool(lib.rdmi_conv2d_in_gn_supported(C.byref(a)))
 
 

@@ -250,7 +250,10 @@ def test_groupnorm_moments_from_gemm(engine):
     (2, 32, 16, 128, 128, False, True, 32), (1, 16, 8, 256, 128, True, False, 32), (3, 16, 32, 320, 256, False, True, 32),
     (1, 16, 16, 1024, 256, False, True, 16), (2, 16, 16, 64, 128, False, True, 8),
     (2, 16, 16, 128, 384, False, True, 32), (1, 16, 16, 256, 640, True, True, 32), (2, 16, 16, 192, 320, False, True, 32),
-    (2, 16, 64, 128, 128, False, True, 32), (1, 16, 32, 256, 128, False, True, 32), (2, 16, 32, 128, 128, False, False, 32)])
+    (2, 16, 64, 128, 128, False, True, 32), (1, 16, 32, 256, 128, False, True, 32), (2, 16, 32, 128, 128, False, False, 32),
+    # Cin > 256 through the scale / shift table (rdmi.h in_affine) on the two-workgroups-per-CU engine
+    (2, 16, 16, 640, 320, False, True, 32), (1, 32, 16, 960, 320, False, True, 32), (2, 16, 16, 512, 128, False, True, 32),
+    (1, 16, 16, 1280, 640, False, True, 32), (1, 8, 8, 512, 512, True, True, 32)])
 def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G, engine, h32):
     """GroupNorm(+SiLU) applied inside the halo conv's input path (rdmi_conv_args.in_*) against the
     unfused groupnorm → conv2d pair on the same data: the same normalised f16 values feed the same

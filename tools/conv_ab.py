@@ -28,6 +28,7 @@ CASES = [
     ("vae 128 768^2 x8 gn", 8, 768, 128, 128, False, "gn"),
     ("vae 128 768^2 x8 plain", 8, 768, 128, 128, False, "plain"),
     ("vae 256->128 768^2 x4 gn", 4, 768, 256, 128, False, "gn"),
+    ("vae 256->128 768^2 x8 full", 8, 768, 256, 128, False, "full"),
     ("vae 256 384^2 x8 full", 8, 384, 256, 256, False, "full"),
     ("vae 512 192^2 x8 plain", 8, 192, 512, 512, False, "plain"),
     ("vae up 256 384->768 x8", 8, 384, 256, 256, True, "plain"),
