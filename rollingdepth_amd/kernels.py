@@ -462,11 +462,13 @@ def gn_conv2d(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
     """conv2d(silu?(GroupNorm(x))): the norm fused into the conv's input path where the halo
     engine runs it and it pays, else groupnorm then conv2d (identical values either way).
     Policy (RDMI_GN_FUSE; tools/kbench.py gnconv on MI355X): 1 (default) fuses for Cin ≤ 256 —
-    the 768²/384² VAE convs, −6…10 % against apply + conv — but not for 512 channels, where the
-    in-conv normalisation costs more than the apply pass it saves (+3…11 %); 2 fuses wherever
-    supported; 0 never."""
+    the 768²/384² VAE convs, −4…16 % against apply + conv — and for Cout ≤ 320, where the halo is
+    normalised by at most three 128-channel output tiles (UNet 960 → 320 / 640 → 320 at 96²: −6 / −4 %,
+    320 → 320 even; profiles/r05e_gnconv_kbench.log), but not for wider outputs, whose every 128-channel
+    tile normalises the same input halo again (512 → 512 at 96²: +14 %, 320 → 640 at 48²: +8 %); 2 fuses
+    wherever supported; 0 never."""
     mode = os.environ.get("RDMI_GN_FUSE", "1")
-    if mode != "0" and (mode == "2" or x.shape[-1] <= 256) and conv2d_in_gn_supported(
+    if mode != "0" and (mode == "2" or x.shape[-1] <= 256 or cout <= 320) and conv2d_in_gn_supported(
             x, w, cout, k, groups, conv_kw.get("stride", 1), conv_kw.get("pad", 1), conv_kw.get("upsample", False),
             conv_kw.get("rowbias"), conv_kw.get("out_hw")):
         mr = groupnorm_stats(x, groups, eps)
