@@ -396,8 +396,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     a.dtype = code
     a.Kp = kp
     aff = None
-    if in_gn is not None and not f32 and Cin > 256 and Cin % 64 == 0:
-        # the norm's scale / shift table for the two-workgroups-per-CU halo engine (rdmi.h in_affine)
+    if in_gn is not None and not f32 and Cin % 64 == 0:
+        # the norm's scale / shift table (rdmi.h in_affine): any Cin on the two-workgroups-per-CU halo
+        # engines, and the double-halo conv_halo_gn8_kernel
         mr, gamma, beta, groups, _ = in_gn
         aff = torch.empty((B, Cin // 64, 2, 64), dtype=F32, device=x.device)
         check(lib.rdmi_groupnorm_affine(mr.data_ptr(), gamma.data_ptr(), beta.data_ptr(), B, Cin, groups,
