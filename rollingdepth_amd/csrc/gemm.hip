@@ -144,13 +144,6 @@ int halo_mode() {
   return he ? atoi(he) : 3;
 }
 
-// conv_halo_gn8_kernel for GroupNorm-input convs given the scale / shift table (RDMI_CONV_GN8, read
-// per launch for A/B: 0 = conv_halo_occ2_kernel instead)
-int gn8_mode() {
-  const char* e = getenv("RDMI_CONV_GN8");
-  return e ? atoi(e) : 1;
-}
-
 // 3×3 s1 p1 (optionally through the ×2 upsample), 64-channel blocks, 16×16 output patches,
 // Cout % 64 == 0 (a ragged last 128-channel tile in the two-workgroups-per-CU variant).
 bool halo_eligible(const rdmi_conv_args* a, int hmode) {
@@ -291,11 +284,6 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     } else if (a->Cout == 128 && (hmode == 4 || (gn && a->Cin > 256 && !p.gaff))) {  // the 8-wave 128-channel variant
       dim3 g(1, patches, 1);
       launch_conv_halo(a->upsample ? 2 : 1, 1, 2, gn, g, st, p);
-    } else if (gn && p.gaff && !a->upsample && a->Ho % 8 == 0 && gn8_mode() != 0) {
-      // the double-halo GroupNorm-input conv (16-wide × 8-tall patches, next block's halo normalised
-      // inside the MFMA stream)
-      dim3 g((a->Cout + 127) / 128, (unsigned)((a->Ho / 8) * (a->Wo / 16) * a->B), 1);
-      launch_conv_gn8(p.gsilu != 0, g, st, p);
     } else if (h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches
       dim3 g(a->Cout / 128, (unsigned)((a->Ho / 8) * (a->Wo / 32) * a->B), 1);
       launch_conv_h32(gn, g, st, p);

@@ -1421,23 +1421,6 @@ __device__ __forceinline__ void occ2_sched(std::integer_sequence<int, S...>) {
   (occ2_sched_one<RN, PD, NS, BPRE, S>(), ...);
 }
 
-// ... and the same with VALU groups between the MFMA groups (conv_halo_gn8_kernel's interleaved
-// transform: 7 VALU after each group of RN MFMAs)
-template <int RN, int PD, int NS, int BPRE, int ST>
-__device__ __forceinline__ void occ2_sched_xf_one() {
-  constexpr int nr = (ST == BPRE ? RN : 0) + (ST + PD < NS ? 1 : 0);
-  if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
-#pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-  }
-}
-template <int RN, int PD, int NS, int BPRE, int... S>
-__device__ __forceinline__ void occ2_sched_xf(std::integer_sequence<int, S...>) {
-  (occ2_sched_xf_one<RN, PD, NS, BPRE, S>(), ...);
-}
-
 // Two-workgroups-per-CU halo conv for 128-channel output tiles (the VAE's 768² convs).  With
 // 128 output channels and Cin = 128 a tile has only 18 K-tiles, so the 8-wave single-workgroup
 // variant above pays its prologue and epilogue un-overlapped on every tile (≈7 µs of ≈27 µs:
@@ -1715,219 +1698,6 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
       o[7] = st_prev;
     }
   }
-}
-
-// GroupNorm-input halo conv with a double halo (round 5).  In
-// conv_halo_occ2_kernel the input's GroupNorm+SiLU is applied to each channel block's halo in a phase
-// of its own (DMA → wait → transform → barrier), during which the wave issues no MFMA: SQ PMC
-// (profiles/r05i_issue_summary.txt) shows 0.065 of the SIMD-cycles with VALU and MFMA executing
-// together and MFMA busy 0.50 against 0.62 for the plain conv.  Here the halo of channel block cb+1 is
-// DMA'd at cb's first tap into a second buffer, and each wave normalises one of its pieces per K-tile
-// (taps 1..6) with the instructions interleaved into the K-tile's MFMA stream
-// (sched_group_barrier), so only channel block 0's transform is a phase of its own.  Two halos of a
-// 16×16 patch do not fit beside the weight ring at two workgroups per CU, so the patch is 16 wide × 8
-// tall: halo 18×10 pixels (24 KiB), two halos + the 2-slot weight ring = 80 KiB, exactly half the CU's
-// LDS.  Workgroup = 4 waves: wm → patch rows 4wm..4wm+3, wn → channels 64wn..+63 (4 × 4 fragments of
-// 16×16, 64 accumulator registers).  K order per output (channel block, tap, k half) and MFMA operands
-// as conv_halo_occ2_kernel: bitwise its results (and the unfused groupnorm → conv pair's).  Needs the
-// scale / shift table p.gaff (rdmi_groupnorm_affine).  SILU: the input's SiLU (a template argument so
-// that the interleaved transform is branch-free).
-template <bool SILU, int STAMP = 0>
-__global__ __launch_bounds__(256, 2) void conv_halo_gn8_kernel(GemmP p) {
-  constexpr int BN = 128, BKP = 64, RM = 4, RN = 4;
-  constexpr int HWD = 18, HRW = 10, HPIX = HWD * HRW;  // 180 halo pixels
-  constexpr int HPW = 6;                    // piece slots per wave: pieces wid + 4e, e < 6 (24 × 8 ≥ 180)
-  constexpr int HALO = 24 * 8 * BKP;        // halves (24 KiB; piece 23 and the tail of 22 are padding)
-  constexpr int BSLOT = BN * BKP;           // halves (16 KiB)
-  constexpr int NB = 4;                     // weight pieces per wave per K-tile
-  __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + 2 * BSLOT];  // 80 KiB
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int wids = __builtin_amdgcn_readfirstlane(wid);
-  const int nbx = gridDim.x;
-  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
-  int mt_, nt_;
-  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
-  const int n0 = nt_ * BN;
-  const int pxn = p.Wo >> 4, pyn = p.Ho >> 3;
-  const int px = mt_ % pxn;
-  const int py = (mt_ / pxn) % pyn;
-  const int b = mt_ / (pxn * pyn);
-  const int y0 = py * 8, x0 = px * 16;
-  const __amdgpu_buffer_rsrc_t ra_ =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rw_ =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.Wt, (short)0, (int)p.w_bytes, 0x00020000);
-
-  const int lrow = lane >> 3;
-  const int chunk = (lane & 7) ^ lrow;
-  unsigned hvo[HPW];  // piece wid + 4e: halo pixel 8(wid + 4e) + lrow — byte offset at channel block 0, or OOB
-  unsigned inm = 0;   // bit e: that pixel lies inside the image (else the conv's zero padding)
-#pragma unroll
-  for (int e = 0; e < HPW; ++e) {
-    const int hp = (wid + 4 * e) * 8 + lrow;
-    const int hr = hp / HWD, hc = hp - hr * HWD;
-    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
-    const bool ok = hp < HPIX && (unsigned)yy < (unsigned)p.IH && (unsigned)xx < (unsigned)p.IW;
-    hvo[e] = ok ? (unsigned)(((b * p.IH + yy) * p.IW + xx) * p.Cin + chunk * 8) * 2u : OOB;
-    inm |= (ok ? 1u : 0u) << e;
-  }
-  unsigned bvo[NB];
-#pragma unroll
-  for (int e = 0; e < NB; ++e) {
-    const int rt = (wid + 4 * e) * 8 + lrow;
-    const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
-    bvo[e] = n < p.N ? (unsigned)(n * (int)p.ldw + chunk * 8) * 2u : OOB;
-  }
-  const int ncb = p.Cin >> 6;
-  auto issueHalo = [&](int cb, int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int e = 0; e < HPW; ++e) dma16s(ra_, hvo[e], cb * 128, lds + buf * HALO + (wids + 4 * e) * 8 * BKP);
-  };
-  auto issueB = [&](int u) __attribute__((always_inline)) {
-    f16* lb = lds + 2 * HALO + (u & 1) * BSLOT;
-#pragma unroll
-    for (int e = 0; e < NB; ++e) dma16s(rw_, bvo[e], u * BKP * 2, lb + (wids + 4 * e) * 8 * BKP);
-  };
-  f32x4 aff[4];  // this lane's 8 scales, 8 shifts of the block being normalised
-  auto loadAff = [&](int cb) __attribute__((always_inline)) {
-    const float* ta = p.gaff + ((long)b * ncb + cb) * 128 + chunk * 8;
-    aff[0] = *(const f32x4*)ta;
-    aff[1] = *(const f32x4*)(ta + 4);
-    aff[2] = *(const f32x4*)(ta + 64);
-    aff[3] = *(const f32x4*)(ta + 68);
-  };
-  // one piece of halo buffer `buf`, in place: gn_apply's arithmetic (fmaf of the f16 value, silu_f,
-  // RNE to f16; bitwise the unfused pass), as builtins rather than gn_xform_words' inline asm so that
-  // the compiler sees every instruction (hazard padding, placement), the padding as a select
-  auto xval = [&](const f16x8& v, int i, bool in) __attribute__((always_inline)) {
-    const float sc = aff[i >> 2][i & 3], sh = aff[2 + (i >> 2)][i & 3];
-    float f = fmaf((float)v[i], sc, sh);
-    if constexpr (SILU) f = silu_f(f);
-    return in ? (f16)f : (f16)0.f;
-  };
-  auto pieceAddr = [&](int buf, int e) __attribute__((always_inline)) {
-    return lds + buf * HALO + (wid + 4 * e) * 8 * BKP + lane * 8;
-  };
-  auto xformPiece = [&](int buf, int e) __attribute__((always_inline)) {
-    f16* lh = pieceAddr(buf, e);
-    const f16x8 v = *(const f16x8*)lh;
-    const bool in = (inm >> e) & 1;
-    f16x8 o;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = xval(v, i, in);
-    *(f16x8*)lh = o;
-  };
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = ncb * 9;
-  const int fr = lane & 15, fq = lane >> 4;
-  const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
-  const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
-
-  // prologue: halo(0) into buffer 0, B(0), block 0's scales / shifts; the block-0 transform
-  issueHalo(0, 0);
-  issueB(0);
-  loadAff(0);
-  wait_vmcnt<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int e = 0; e < HPW; ++e) xformPiece(0, e);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  const int wms = __builtin_amdgcn_readfirstlane(wm);
-  const bool live = n0 + (wids & 1) * 64 < p.N;  // wave-uniform
-  // one K-tile: fragment reads software-pipelined two MFMA groups ahead (as conv_halo_occ2_kernel).
-  // XF: the K-tile also normalises piece e of the next block's halo (buffer nbuf): the piece is read
-  // with the first fragments, and after MFMA group st (4 MFMAs, 64 matrix cycles) its value st is
-  // transformed — a 7-instruction dependent chain issued while those MFMAs execute — the order pinned
-  // by sched_barrier fences; the piece is written back after the last group.
-  auto ktile = [&](int u, int cb, int tap, auto XFc, int nbuf, int e) __attribute__((always_inline)) {
-    constexpr bool XF = decltype(XFc)::value;
-    const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
-    const f16* lb = lds + 2 * HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
-    const int xb = fr + dx + 2 * dy;
-    const unsigned abase = (unsigned)(((cb & 1) * HALO + ((wms * RM + dy) * HWD + dx + fr) * BKP) * 2);
-    unsigned aoff[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) aoff[r] = abase + (unsigned)((fq ^ ((xb + 2 * r) & 7)) << 4);
-    auto readA = [&](int kh, int i) __attribute__((always_inline)) {
-      const unsigned a = kh ? (aoff[i] ^ 64u) : aoff[i];
-      return *(const f16x8*)((const char*)lds + a);
-    };
-    f16x8 pv = {}, po;
-    bool pin = false;
-    if constexpr (XF) {
-      pv = *(const f16x8*)pieceAddr(nbuf, e);
-      pin = (inm >> e) & 1;
-    }
-    if (live) {
-      constexpr int NS = 2 * RM, PD = 2, BPRE = RM - 3;
-      f16x8 bfr[2][RN], ar[PD + 1];
-#pragma unroll
-      for (int j = 0; j < RN; ++j) bfr[0][j] = *(const f16x8*)(lb + j * 16 * BKP + off0);
-#pragma unroll
-      for (int q = 0; q < PD; ++q) ar[q] = readA(q / RM, q % RM);
-#pragma unroll
-      for (int st = 0; st < NS; ++st) {
-        if (st == BPRE) {
-#pragma unroll
-          for (int j = 0; j < RN; ++j) bfr[1][j] = *(const f16x8*)(lb + j * 16 * BKP + off1);
-        }
-        if (st + PD < NS) ar[(st + PD) % (PD + 1)] = readA((st + PD) / RM, (st + PD) % RM);
-        const int kh = st / RM, i = st % RM;
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[kh][j], ar[st % (PD + 1)], acc[i][j], 0, 0, 0);
-        if constexpr (XF) {
-          __builtin_amdgcn_sched_barrier(0);
-          po[st] = xval(pv, st, pin);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    } else if constexpr (XF) {  // a wave past N still normalises its pieces for the others
-#pragma unroll
-      for (int i = 0; i < 8; ++i) po[i] = xval(pv, i, pin);
-    }
-    if constexpr (XF) *(f16x8*)pieceAddr(nbuf, e) = po;
-  };
-
-  for (int u = 0; u < nk; ++u) {
-    const int cb = u / 9;
-    const int tap = u - cb * 9;
-    if (u > 0) {
-      wait_vmcnt<0>();  // B(u) (and, at tap 1, the next block's halo pieces and scales / shifts)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own reads of K-tile u-1 (and transform writes) done
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-    const bool nxt = cb + 1 < ncb;
-    if (tap == 0 && nxt) {  // halo(cb+1) into the other buffer (last read in block cb-1)
-      issueHalo(cb + 1, (cb + 1) & 1);
-      loadAff(cb + 1);
-    }
-    if (u + 1 < nk) issueB(u + 1);
-    if (nxt && tap >= 1 && tap <= HPW)
-      ktile(u, cb, tap, std::true_type{}, (cb + 1) & 1, tap - 1);
-    else
-      ktile(u, cb, tap, std::false_type{}, 0, 0);
-  }
-  if (live)
-    store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq,
-                                 p.cperm);
-  wait_vmcnt<0>();  // drain trailing DMAs before the workgroup can retire
 }
 
 // Halo conv with 32×32×16 MFMAs for 128-channel output tiles (the VAE's 768² / 384² convs with
@@ -2430,6 +2200,5 @@ void launch_gemm_occ2(int bn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_halo(int mode, int nph, int wn, bool gn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_occ2(int mode, bool gn, bool pipe, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_h32(bool gn, dim3 g, hipStream_t s, const GemmP& p);
-void launch_conv_gn8(bool silu, dim3 g, hipStream_t s, const GemmP& p);
 
 }  // namespace rdmi_gk

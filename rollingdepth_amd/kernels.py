@@ -398,7 +398,9 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     aff = None
     if in_gn is not None and not f32 and Cin % 64 == 0:
         # the norm's scale / shift table (rdmi.h in_affine): any Cin on the two-workgroups-per-CU halo
-        # engines, and the double-halo conv_halo_gn8_kernel
+        # engine, each wave's 8 + 8 values loaded with the halo refill (for Cin <= 256 too: −2…4 %
+        # against the LDS table built in the prologue, profiles/r05j_gn8_ab.log RDMI_CONV_GN8=0 columns
+        # against r05b_h32_ab.log RDMI_CONV_H32=0)
         mr, gamma, beta, groups, _ = in_gn
         aff = torch.empty((B, Cin // 64, 2, 64), dtype=F32, device=x.device)
         check(lib.rdmi_groupnorm_affine(mr.data_ptr(), gamma.data_ptr(), beta.data_ptr(), B, Cin, groups,
