@@ -54,6 +54,7 @@ PEAK_F32_TFLOPS = 157.3   # MI355X f32-input MFMA (= f32 vector peak)
 # the bf16-split f32 engine (RDMI_F32_X3) spends three bf16 MFMA products per f32 multiply-add: its
 # ceiling in f32 flops is the bf16 peak / 3
 PEAK_F32X3_TFLOPS = PEAK_F16_TFLOPS / 3
+PEAK_F32X6_TFLOPS = PEAK_F16_TFLOPS / 6  # the three-way split (RDMI_F32_X6): six bf16 products per f32 MAC
 PEAK_HBM_GBS = 8000.0
 
 # run_video.py:413-452 presets (BASELINE.json configs[1..4])
@@ -446,7 +447,7 @@ def main():
         p = prof[dom]
         ach = _fam(dom)
         peak = (PEAK_F32_TFLOPS if dom.endswith("_f32") else PEAK_F32X3_TFLOPS if dom.endswith("_f32x3")
-                else PEAK_F16_TFLOPS)
+                else PEAK_F32X6_TFLOPS if dom.endswith("_f32x6") else PEAK_F16_TFLOPS)
         tr = _pmc_traffic(a.preset, dom)
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 1), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": tr and round(tr["bytes_per_launch"]),
@@ -456,7 +457,7 @@ def main():
                 "per_kernel": {k: {"tflops": round(_fam(k), 1), "ms": round(v["ms"], 1), "launches": v["n"]}
                                for k, v in prof.items()}}
         for an, apk in (("attention_fwd", PEAK_F16_TFLOPS), ("attention_fwd_f32", PEAK_F32_TFLOPS),
-                        ("attention_fwd_f32x3", PEAK_F32X3_TFLOPS)):
+                        ("attention_fwd_f32x3", PEAK_F32X3_TFLOPS), ("attention_fwd_f32x6", PEAK_F32X6_TFLOPS)):
             if an in prof:
                 att = _fam(an)
                 roof["attention"] = {"kernel": an, "achieved": round(att, 1), "peak": apk, "unit": "TFLOP/s",

@@ -38,6 +38,11 @@ extern "C" {
  * products a_hi·w_hi + a_hi·w_lo + a_lo·w_hi on the bf16 MFMA with f32 accumulation (≈2^-16 relative
  * error per product; the paper preset's fast f32 engine, RDMI_F32_X3=1 in rollingdepth_amd) */
 #define RDMI_F32_X3 3
+/* rdmi_attention_fwd (round 5): f32 q/k/v/o and softmax, both products on the bf16 MFMA over a three-way
+ * bf16 split of each f32 operand (hi + mid + lo, six partial products kept): a few 2^-24 relative per
+ * product — f32's own product rounding, the reference's exact-fp32 SDPA precision — at ≈0.4 of the
+ * exact f32-input MFMA's matrix time */
+#define RDMI_F32_X6 4
 
 /* rdmi_resize modes: torchvision InterpolationMode NEAREST / BILINEAR / BICUBIC */
 #define RDMI_RESIZE_NEAREST 0
@@ -180,7 +185,8 @@ int rdmi_layernorm(const void* x, void* y, int dtype, long M, int C, const float
 /* ---------------------------------------------------------------------------------------
  * Fused multi-head attention forward, softmax(q kᵀ · scale) v, non-causal, no mask, D = 64; dtype
  * RDMI_F16 (f16 MFMA, f32 softmax), RDMI_F32 (f32-input MFMA, f32 softmax; the paper preset) or
- * RDMI_F32_X3 (f32 q/k/v/o and softmax, both products as bf16-split triples on the bf16 MFMA).
+ * RDMI_F32_X3 (f32 q/k/v/o and softmax, both products as bf16-split triples on the bf16 MFMA) or
+ * RDMI_F32_X6 (the same with three-part splits and six products: f32-equivalent products).
  * Token-major q/k/v/o with row strides (ld*) and batch strides (bs*), head h at column h*D.
  * With the num_view fold done by the caller's strides (one "batch" = one snippet of n frames,
  * S = n·h·w), this is the cross-frame self-attention of the modified AttnProcessor2_0

@@ -115,7 +115,7 @@ _SIGS = {
                                                i32, C.POINTER(i32), C.POINTER(i32), vp, vp, vp]),
 }
 
-RDMI_F16, RDMI_F32, RDMI_U8, RDMI_F32_X3 = 0, 1, 2, 3
+RDMI_F16, RDMI_F32, RDMI_U8, RDMI_F32_X3, RDMI_F32_X6 = 0, 1, 2, 3, 4
 RDMI_RESIZE_NEAREST, RDMI_RESIZE_BILINEAR, RDMI_RESIZE_BICUBIC = 0, 1, 2
 
 EXPORTED = tuple(_SIGS)

@@ -1029,9 +1029,9 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
   RDMI_REQUIRE(q && k && v && o, RDMI_E_ARG, "attention_fwd: null pointer");
   RDMI_REQUIRE(D == 64, RDMI_E_UNSUPPORTED, "attention_fwd: head_dim %d unsupported (64 only)", D);
   RDMI_REQUIRE(B > 0 && H > 0 && Sq > 0 && Sk > 0, RDMI_E_ARG, "attention_fwd: bad sizes");
-  if (dtype == RDMI_F32 || dtype == RDMI_F32_X3)
+  if (dtype == RDMI_F32 || dtype == RDMI_F32_X3 || dtype == RDMI_F32_X6)
     return rdmi::attention_fwd_f32(q, k, v, o, B, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs, scale,
-                                   dtype == RDMI_F32_X3, stream);
+                                   dtype == RDMI_F32_X3 ? 2 : dtype == RDMI_F32_X6 ? 3 : 1, stream);
   RDMI_REQUIRE(q_ld % 8 == 0 && k_ld % 8 == 0 && v_ld % 8 == 0 && o_ld % 4 == 0 && (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) & 15) == 0,
                RDMI_E_ALIGN, "attention_fwd: strides/pointers must be 16-byte aligned");
   AttnP p{(const f16*)q, (const f16*)k, (const f16*)v, (f16*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs,

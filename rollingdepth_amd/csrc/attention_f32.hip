@@ -1,6 +1,6 @@
 // f32 cross-frame flash attention (the paper preset's fp32 SDPA, attention_processor.py:2251-2253,
-// behind rdmi_attention_fwd with dtype RDMI_F32, exact products; RDMI_F32_X3: bf16-split products,
-// attn_fwd_f32x3 below).  head_dim 64, non-causal, no mask.
+// behind rdmi_attention_fwd with dtype RDMI_F32, exact products; RDMI_F32_X3 / RDMI_F32_X6: bf16-split
+// products, attn_fwd_f32s below).  head_dim 64, non-causal, no mask.
 //
 // gfx950 runs f32 matrix products only on v_mfma_f32_16x16x4_f32 (exact f32, 1/16 of the f16 rate),
 // so this kernel is MFMA-bound by a wide margin and its design goal is to keep the matrix pipe fed:
@@ -196,12 +196,17 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32(AttnF32P p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// X3 form (dtype RDMI_F32_X3): the same flash schedule with both products on
-// v_mfma_f32_16x16x32_bf16 as bf16-split triples (a·b ≈ a_hi·b_hi + a_lo·b_hi + a_hi·b_lo, rdmi.h):
-// 6 bf16 MFMAs per 16×16×64 block where the exact form spends 16 f32 ones (each twice as long).
-//   * K and V are split once per workgroup as the tiles are staged: K as [key][d] hi and lo planes
-//     (128-B rows, 16-B chunks XOR-swizzled by key & 7), V transposed into [d][key] hi and lo planes
-//     (row stride 68 bf16), so every fragment read is one ds_read_b128 (K) or two ds_read_b64 (V);
+// Split forms: the same flash schedule with both products on v_mfma_f32_16x16x32_bf16 over bf16
+// parts of the f32 operands.  NP = 2 (dtype RDMI_F32_X3, the bf16x3 products of rdmi.h):
+// a·b ≈ a_hi·b_hi + a_lo·b_hi + a_hi·b_lo, ≈2^-16 relative per product — 6 bf16 MFMAs per 16×16×64
+// block where the exact form spends 16 f32 ones (each twice as long).  NP = 3 (RDMI_F32_X6, round 5):
+// three parts, x = x_hi + x_mid + x_lo + O(2^-26 |x|), and the six products whose parts' orders sum
+// to ≤ 2 (hi·hi, mid·hi, hi·mid, mid·mid, lo·hi, hi·lo): the dropped terms and the splits leave a few
+// 2^-24 per product — f32's own product rounding, i.e. the reference's exact-fp32 matmul / SDPA
+// precision — at 12 bf16 MFMAs per block (≈0.4 of the exact form's matrix time).
+//   * K and V are split once per workgroup as the tiles are staged: K as [key][d] planes (128-B rows,
+//     16-B chunks XOR-swizzled by key & 7), V transposed into [d][key] planes (row stride 68 bf16),
+//     so every fragment read is one ds_read_b128 (K) or two ds_read_b64 (V);
 //   * Q (prescaled by scale·log2 e in f32) is split once into registers;
 //   * Sᵀ keeps the exact form's lane layout (query on the lane, keys 4(l >> 4) + r of each 16-key
 //     fragment), so the online softmax is unchanged; P is split per 32-key step, its k slots
@@ -210,9 +215,53 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32(AttnF32P p) {
 constexpr int KR3 = 64;  // bf16 per K plane row
 constexpr int VT3 = 68;  // bf16 per Vᵀ plane row (34 dwords)
 
-__global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
-  __shared__ __attribute__((aligned(16))) unsigned short kp[2][2][KT * KR3];  // [slot][hi, lo]
-  __shared__ __attribute__((aligned(16))) unsigned short vp[2][2][64 * VT3];
+// the products kept: (part of the LDS operand, part of the register operand), largest first
+template <int NP>
+struct SplitProducts;
+template <>
+struct SplitProducts<2> {
+  static constexpr int N = 3;
+  static constexpr int a[3] = {0, 1, 0}, b[3] = {0, 0, 1};
+};
+template <>
+struct SplitProducts<3> {
+  static constexpr int N = 6;
+  static constexpr int a[6] = {0, 1, 0, 1, 2, 0}, b[6] = {0, 0, 1, 1, 0, 2};
+};
+
+// 8 f32 values (a0 then a1) → NP bf16x8 parts
+template <int NP>
+__device__ __forceinline__ void splitN_bf16x8(const f32x4& a0, const f32x4& a1, bf16x8 (&o)[NP]) {
+  if constexpr (NP == 2) {
+    rdmi::split_bf16x8(a0, a1, o[0], o[1]);
+  } else {
+    unsigned h[4], m[4], l[4];
+    rdmi::split3_bf16x2(a0[0], a0[1], h[0], m[0], l[0]);
+    rdmi::split3_bf16x2(a0[2], a0[3], h[1], m[1], l[1]);
+    rdmi::split3_bf16x2(a1[0], a1[1], h[2], m[2], l[2]);
+    rdmi::split3_bf16x2(a1[2], a1[3], h[3], m[3], l[3]);
+    o[0] = __builtin_bit_cast(bf16x8, u32x4{h[0], h[1], h[2], h[3]});
+    o[1] = __builtin_bit_cast(bf16x8, u32x4{m[0], m[1], m[2], m[3]});
+    o[2] = __builtin_bit_cast(bf16x8, u32x4{l[0], l[1], l[2], l[3]});
+  }
+}
+// two f32 values → NP packed bf16 pairs
+template <int NP>
+__device__ __forceinline__ void splitN_bf16x2(float x0, float x1, unsigned (&o)[NP]) {
+  if constexpr (NP == 2) {
+    const u32x2 t = rdmi::split_bf16x2(x0, x1);
+    o[0] = t[0];
+    o[1] = t[1];
+  } else {
+    rdmi::split3_bf16x2(x0, x1, o[0], o[1], o[2]);
+  }
+}
+
+template <int NP>
+__global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32s(AttnF32P p) {
+  using PR = SplitProducts<NP>;
+  __shared__ __attribute__((aligned(16))) unsigned short kp[2][NP][KT * KR3];  // [slot][part]
+  __shared__ __attribute__((aligned(16))) unsigned short vp[2][NP][64 * VT3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, qq = lane >> 4;
   const int head = blockIdx.y, b = blockIdx.z;
@@ -222,7 +271,7 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
   const float* Vg = p.v + (long)b * p.v_bs + head * 64;
 
   // Q fragments: step t holds Q[q0 + 16f + fr][32t + 8qq .. +7] · scale·log2(e), split
-  bf16x8 qh[QF][2], ql[QF][2];
+  bf16x8 qs[QF][2][NP];
 #pragma unroll
   for (int f = 0; f < QF; ++f) {
     const int qi = q0 + 16 * f + fr;
@@ -233,7 +282,7 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
         x0 = *(const f32x4*)(Q + (long)qi * p.q_ld + 32 * t + 8 * qq) * p.sl2;
         x1 = *(const f32x4*)(Q + (long)qi * p.q_ld + 32 * t + 8 * qq + 4) * p.sl2;
       }
-      rdmi::split_bf16x8(x0, x1, qh[f][t], ql[f][t]);
+      splitN_bf16x8<NP>(x0, x1, qs[f][t]);
     }
   }
 
@@ -254,25 +303,26 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
   };
   auto lstore = [&](int slot) {
     const int ch = tid & 15, row0 = 2 * (tid >> 4);
-    u32x2 vh[LPT], vl[LPT];
+    unsigned vs[LPT][2][NP];  // [row][d pair][part]: d 4ch..4ch+3 of key row0 + i as bf16 pairs
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int row = row0 + i;  // key row, d = 4ch .. 4ch+3
-      u32x2 s0 = rdmi::split_bf16x2(kr[i][0], kr[i][1]), s1 = rdmi::split_bf16x2(kr[i][2], kr[i][3]);
+      unsigned s0[NP], s1[NP];
+      splitN_bf16x2<NP>(kr[i][0], kr[i][1], s0);
+      splitN_bf16x2<NP>(kr[i][2], kr[i][3], s1);
       const int ko = row * KR3 + (((ch >> 1) ^ (row & 7)) << 3) + (ch & 1) * 4;
-      *(u32x2*)&kp[slot][0][ko] = u32x2{s0[0], s1[0]};
-      *(u32x2*)&kp[slot][1][ko] = u32x2{s0[1], s1[1]};
-      s0 = rdmi::split_bf16x2(vr[i][0], vr[i][1]);
-      s1 = rdmi::split_bf16x2(vr[i][2], vr[i][3]);
-      vh[i] = u32x2{s0[0], s1[0]};  // d 4ch..4ch+3 of key row0 + i, bf16 pairs
-      vl[i] = u32x2{s0[1], s1[1]};
+#pragma unroll
+      for (int q = 0; q < NP; ++q) *(u32x2*)&kp[slot][q][ko] = u32x2{s0[q], s1[q]};
+      splitN_bf16x2<NP>(vr[i][0], vr[i][1], vs[i][0]);
+      splitN_bf16x2<NP>(vr[i][2], vr[i][3], vs[i][1]);
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {  // Vᵀ[d][row0], Vᵀ[d][row0 + 1] as one 32-bit store per plane
       const int vo = (4 * ch + e) * VT3 + row0;
       const unsigned sh = 16 * (e & 1);
-      *(unsigned*)&vp[slot][0][vo] = ((vh[0][e >> 1] >> sh) & 0xFFFFu) | ((vh[1][e >> 1] >> sh) << 16);
-      *(unsigned*)&vp[slot][1][vo] = ((vl[0][e >> 1] >> sh) & 0xFFFFu) | ((vl[1][e >> 1] >> sh) << 16);
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        *(unsigned*)&vp[slot][q][vo] = ((vs[0][e >> 1][q] >> sh) & 0xFFFFu) | ((vs[1][e >> 1][q] >> sh) << 16);
     }
   };
 
@@ -300,10 +350,6 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
       lstore(slot ^ 1);
       if (kt + 2 < nkt) gload(kt + 2);
     }
-    const unsigned short* kh = kp[slot][0];
-    const unsigned short* kl = kp[slot][1];
-    const unsigned short* vh = vp[slot][0];
-    const unsigned short* vl = vp[slot][1];
     // Sᵀ = K·Qᵀ
     f32x4 s[QF][KFR];
 #pragma unroll
@@ -316,13 +362,14 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int off = row * KR3 + (((4 * t + qq) ^ (row & 7)) << 3);
-        const bf16x8 ah = *(const bf16x8*)(kh + off), al = *(const bf16x8*)(kl + off);
+        bf16x8 ka[NP];
 #pragma unroll
-        for (int f = 0; f < QF; ++f) {
-          s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, qh[f][t], s[f][g], 0, 0, 0);
-          s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, qh[f][t], s[f][g], 0, 0, 0);
-          s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, ql[f][t], s[f][g], 0, 0, 0);
-        }
+        for (int q = 0; q < NP; ++q) ka[q] = *(const bf16x8*)(kp[slot][q] + off);
+#pragma unroll
+        for (int f = 0; f < QF; ++f)
+#pragma unroll
+          for (int j = 0; j < PR::N; ++j)
+            s[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka[PR::a[j]], qs[f][t][PR::b[j]], s[f][g], 0, 0, 0);
       }
     }
     if ((kt + 1) * KT > p.Sk) {
@@ -363,22 +410,23 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32x3(AttnF32P p) {
     // Oᵀ += Vᵀ·Pᵀ in two 32-key steps
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      bf16x8 ph[QF], pl[QF];
+      bf16x8 ps[QF][NP];
 #pragma unroll
-      for (int f = 0; f < QF; ++f) rdmi::split_bf16x8(s[f][2 * u], s[f][2 * u + 1], ph[f], pl[f]);
+      for (int f = 0; f < QF; ++f) splitN_bf16x8<NP>(s[f][2 * u], s[f][2 * u + 1], ps[f]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int vo = (16 * e + fr) * VT3 + 32 * u + 4 * qq;
-        const u32x2 h0 = *(const u32x2*)(vh + vo), h1 = *(const u32x2*)(vh + vo + 16);
-        const u32x2 l0 = *(const u32x2*)(vl + vo), l1 = *(const u32x2*)(vl + vo + 16);
-        const bf16x8 bh = __builtin_bit_cast(bf16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
-        const bf16x8 bl = __builtin_bit_cast(bf16x8, u32x4{l0[0], l0[1], l1[0], l1[1]});
+        bf16x8 va[NP];
 #pragma unroll
-        for (int f = 0; f < QF; ++f) {
-          o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ph[f], o[f][e], 0, 0, 0);
-          o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ph[f], o[f][e], 0, 0, 0);
-          o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, pl[f], o[f][e], 0, 0, 0);
+        for (int q = 0; q < NP; ++q) {
+          const u32x2 h0 = *(const u32x2*)(vp[slot][q] + vo), h1 = *(const u32x2*)(vp[slot][q] + vo + 16);
+          va[q] = __builtin_bit_cast(bf16x8, u32x4{h0[0], h0[1], h1[0], h1[1]});
         }
+#pragma unroll
+        for (int f = 0; f < QF; ++f)
+#pragma unroll
+          for (int j = 0; j < PR::N; ++j)
+            o[f][e] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va[PR::a[j]], ps[f][PR::b[j]], o[f][e], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -404,16 +452,20 @@ namespace rdmi {
 
 int attention_fwd_f32(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, long q_ld,
                       long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs, long o_bs, float scale,
-                      bool x3, void* stream) {
+                      int parts, void* stream) {
   RDMI_REQUIRE(q_ld % 4 == 0 && k_ld % 4 == 0 && v_ld % 4 == 0 && o_ld % 4 == 0 &&
                    ((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o) & 15) == 0),
                RDMI_E_ALIGN, "attention_fwd f32: strides/pointers must be 16-byte aligned");
   AttnF32P p{(const float*)q, (const float*)k, (const float*)v, (float*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld,
              q_bs, k_bs, v_bs, o_bs, scale * 1.4426950408889634f};
   dim3 g(rdmi::div_up(Sq, QBF), H, B);
-  if (x3) {
-    hipLaunchKernelGGL(attn_fwd_f32x3, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
+  if (parts == 2) {
+    hipLaunchKernelGGL(attn_fwd_f32s<2>, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
     return rdmi::check_launch("attention_fwd f32x3");
+  }
+  if (parts == 3) {
+    hipLaunchKernelGGL(attn_fwd_f32s<3>, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
+    return rdmi::check_launch("attention_fwd f32x6");
   }
   hipLaunchKernelGGL(attn_fwd_f32, g, dim3(64 * NWF), 0, (hipStream_t)stream, p);
   return rdmi::check_launch("attention_fwd f32");

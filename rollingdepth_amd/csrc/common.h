@@ -36,7 +36,7 @@ int conv2d_f32(const rdmi_conv_args* a, void* stream);
 // f32 flash attention behind rdmi_attention_fwd (attention_f32.hip)
 int attention_fwd_f32(const void* q, const void* k, const void* v, void* o, int B, int H, int Sq, int Sk, long q_ld,
                       long k_ld, long v_ld, long o_ld, long q_bs, long k_bs, long v_bs, long o_bs, float scale,
-                      bool x3, void* stream);
+                      int parts, void* stream);  // parts: 1 exact f32, 2 bf16x3, 3 bf16x6
 
 inline int div_up(long a, long b) { return (int)((a + b - 1) / b); }
 
@@ -80,6 +80,16 @@ __device__ __forceinline__ u32x2 split_bf16x2(float x0, float x1) {  // {hi, lo}
   const float r0 = x0 - __builtin_bit_cast(float, hi << 16), r1 = x1 - __builtin_bit_cast(float, hi & 0xffff0000u);
   asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(lo) : "v"(r0), "v"(r1));
   return u32x2{hi, lo};
+}
+
+// Two f32 values → packed bf16 hi, mid and lo parts (each remainder exact in f32, each part RNE):
+// x = x_hi + x_mid + x_lo + O(2^-26 |x|) — the three-way split of the f32 engines' x6 products.
+__device__ __forceinline__ void split3_bf16x2(float x0, float x1, unsigned& hi, unsigned& mid, unsigned& lo) {
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(hi) : "v"(x0), "v"(x1));
+  const float r0 = x0 - __builtin_bit_cast(float, hi << 16), r1 = x1 - __builtin_bit_cast(float, hi & 0xffff0000u);
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(mid) : "v"(r0), "v"(r1));
+  const float t0 = r0 - __builtin_bit_cast(float, mid << 16), t1 = r1 - __builtin_bit_cast(float, mid & 0xffff0000u);
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(lo) : "v"(t0), "v"(t1));
 }
 
 // 8 f32 values (a0 then a1) → bf16x8 hi and lo parts

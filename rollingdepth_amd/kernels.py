@@ -117,10 +117,21 @@ def f32_x3(kind: str = "conv") -> bool:
     return m == "1" or (m == "conv" and kind == "conv")
 
 
+def f32_x6() -> bool:
+    """Whether the f32 path's cross-frame attention (with RDMI_F32_X3=conv) runs its products on the
+    three-way bf16 split (RDMI_F32_X6, rdmi.h: six bf16 MFMA products per f32 multiply-add, a few 2^-24
+    per product — f32's own product rounding) instead of the exact f32-input MFMA: the same precision
+    class at ≈2.5× the matrix rate.  RDMI_F32_X6=0 keeps the exact engine.  Read per attention call."""
+    return _f32_x3_mode() == "conv" and os.environ.get("RDMI_F32_X6", "1") != "0"
+
+
 def f32_precision_label() -> str:
     """The f32 path's product precision, for bench lines."""
-    return {"0": "exact f32 products", "conv": "bf16x3 conv products, exact f32 Linear/attention",
-            "1": "bf16x3 products"}[_f32_x3_mode()]
+    m = _f32_x3_mode()
+    if m == "conv":
+        return "bf16x3 conv products, exact f32 Linear, " + \
+            ("f32-equivalent bf16x6 attention products" if f32_x6() else "exact f32 attention")
+    return {"0": "exact f32 products", "1": "bf16x3 products"}[m]
 
 
 def split_bf16(w: torch.Tensor) -> torch.Tensor:
@@ -578,8 +589,11 @@ def attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, out
     sc = 1.0 / math.sqrt(D) if scale is None else scale
     code = _dtype_code(q)
     if code == _N.RDMI_F32 and f32_x3("linear"):
-        code = _N.RDMI_F32_X3  # bf16-split products (attention_f32.hip attn_fwd_f32x3)
-    name = {_N.RDMI_F16: "attention_fwd", _N.RDMI_F32: "attention_fwd_f32", _N.RDMI_F32_X3: "attention_fwd_f32x3"}[code]
+        code = _N.RDMI_F32_X3  # bf16-split products (attention_f32.hip attn_fwd_f32s<2>)
+    elif code == _N.RDMI_F32 and f32_x6():
+        code = _N.RDMI_F32_X6  # three-way split, f32-equivalent products (attn_fwd_f32s<3>)
+    name = {_N.RDMI_F16: "attention_fwd", _N.RDMI_F32: "attention_fwd_f32", _N.RDMI_F32_X3: "attention_fwd_f32x3",
+            _N.RDMI_F32_X6: "attention_fwd_f32x6"}[code]
     es = q.element_size()
     with _Timed(name, 4.0 * B * heads * Sq * Sk * D, f"attn B={B} H={heads} S={Sq}",
                 es * B * heads * D * (2 * Sq + 2 * Sk)):
