@@ -475,14 +475,16 @@ def gn_conv2d(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
               w: torch.Tensor, cout: int, k: int, **conv_kw) -> torch.Tensor:
     """conv2d(silu?(GroupNorm(x))): the norm fused into the conv's input path where the halo
     engine runs it and it pays, else groupnorm then conv2d (identical values either way).
-    Policy (RDMI_GN_FUSE; tools/kbench.py gnconv on MI355X): 1 (default) fuses for Cin ≤ 256 —
-    the 768²/384² VAE convs, −4…16 % against apply + conv — and for Cout ≤ 320, where the halo is
-    normalised by at most three 128-channel output tiles (UNet 960 → 320 / 640 → 320 at 96²: −6 / −4 %,
-    320 → 320 even; profiles/r05e_gnconv_kbench.log), but not for wider outputs, whose every 128-channel
-    tile normalises the same input halo again (512 → 512 at 96²: +14 %, 320 → 640 at 48²: +8 %); 2 fuses
-    wherever supported; 0 never."""
+    Policy (RDMI_GN_FUSE; tools/kbench.py gnconv on MI355X): 1 (default) fuses for Cin ≤ 256 — the
+    768²/384² VAE convs, −4…16 % against apply + conv; wider inputs (any Cin since round 5, through
+    the scale / shift table) stay unfused: every 128-channel output tile normalises the same input
+    halo again (512 → 512 at 96²: +14 %, 320 → 640 at 48²: +8 %, profiles/r05e_gnconv_kbench.log), and
+    at the pipeline's 75-frame batches also where kbench's 24/48-frame cases broke even or won — the
+    fused 96² 320 → 320, 640 → 320 and 384² 512 → 256 convs cost 6 + 4 + 23 ms a step more than the
+    apply passes they saved (29 ms, profiles/r05n_shapes.log against r04au); 2 fuses wherever
+    supported; 0 never."""
     mode = os.environ.get("RDMI_GN_FUSE", "1")
-    if mode != "0" and (mode == "2" or x.shape[-1] <= 256 or cout <= 320) and conv2d_in_gn_supported(
+    if mode != "0" and (mode == "2" or x.shape[-1] <= 256) and conv2d_in_gn_supported(
             x, w, cout, k, groups, conv_kw.get("stride", 1), conv_kw.get("pad", 1), conv_kw.get("upsample", False),
             conv_kw.get("rowbias"), conv_kw.get("out_hw")):
         mr = groupnorm_stats(x, groups, eps)

@@ -21,7 +21,8 @@ import re
 FAMILIES = [
     ("implicit_gemm_f32x3", re.compile(r"gemm_f32_kernel<\d+, true>|gemm_f32_kernelILi\dELb1E")),
     ("implicit_gemm_f32", re.compile(r"gemm_f32_kernel")),
-    ("attention_fwd_f32x3", re.compile(r"attn_fwd_f32x3")),
+    ("attention_fwd_f32x6", re.compile(r"attn_fwd_f32s<3>|attn_fwd_f32sILi3E")),
+    ("attention_fwd_f32x3", re.compile(r"attn_fwd_f32x3|attn_fwd_f32s<2>|attn_fwd_f32sILi2E")),
     ("attention_fwd_f32", re.compile(r"attn_fwd_f32")),
     ("implicit_gemm", re.compile(r"conv_halo_kernel|conv_halo_occ2_kernel|gemm_pp_kernel|gemm_occ2_kernel|gemm_kernel<")),
     ("attention_fwd", re.compile(r"attn_fwd_d64")),
