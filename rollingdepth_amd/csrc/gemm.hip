@@ -183,8 +183,8 @@ extern "C" int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* a) {
 extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
   RDMI_REQUIRE(a && a->A && a->W && a->C, RDMI_E_ARG, "gemm: null pointer");
   RDMI_REQUIRE(a->M > 0 && a->N > 0 && a->K > 0 && a->batch > 0, RDMI_E_ARG, "gemm: bad sizes M=%d N=%d K=%d", a->M, a->N, a->K);
-  RDMI_REQUIRE(a->dtype == RDMI_F16 || a->dtype == RDMI_F32 || a->dtype == RDMI_F32_X3, RDMI_E_UNSUPPORTED,
-               "gemm: dtype %d", a->dtype);
+  RDMI_REQUIRE(a->dtype == RDMI_F16 || a->dtype == RDMI_F32 || a->dtype == RDMI_F32_X3 || a->dtype == RDMI_F32_X6,
+               RDMI_E_UNSUPPORTED, "gemm: dtype %d", a->dtype);
   if (a->dtype != RDMI_F16) return rdmi::gemm_f32(a, stream);
   RDMI_REQUIRE(a->K % 8 == 0 && a->lda % 8 == 0 && a->ldw % 8 == 0 && a->ldw >= a->K,
                RDMI_E_ALIGN, "gemm: K (%d), lda (%ld) must be multiples of 8 and ldw (%ld) >= K", a->K, a->lda, a->ldw);
@@ -217,8 +217,8 @@ extern "C" int rdmi_gemm(const rdmi_gemm_args* a, void* stream) {
 extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   RDMI_REQUIRE(a && a->x && a->w && a->y, RDMI_E_ARG, "conv2d: null pointer");
   RDMI_REQUIRE(a->B > 0 && a->H > 0 && a->W > 0 && a->Cout > 0 && a->Ho > 0 && a->Wo > 0, RDMI_E_ARG, "conv2d: bad sizes");
-  RDMI_REQUIRE(a->dtype == RDMI_F16 || a->dtype == RDMI_F32 || a->dtype == RDMI_F32_X3, RDMI_E_UNSUPPORTED,
-               "conv2d: dtype %d", a->dtype);
+  RDMI_REQUIRE(a->dtype == RDMI_F16 || a->dtype == RDMI_F32 || a->dtype == RDMI_F32_X3 || a->dtype == RDMI_F32_X6,
+               RDMI_E_UNSUPPORTED, "conv2d: dtype %d", a->dtype);
   if (a->dtype != RDMI_F16) return rdmi::conv2d_f32(a, stream);
   RDMI_REQUIRE(a->Cin % 8 == 0, RDMI_E_ALIGN, "conv2d: Cin (%d) must be a multiple of 8", a->Cin);
   const int K = a->kh * a->kw * a->Cin;

@@ -24,6 +24,14 @@
 // 2^-11 for the TF32 that cuDNN's fp32 convolutions use by default on the reference's Ampere GPU).
 // The weight rows hold, per 32-deep K-tile, 32 bf16 hi then 32 bf16 lo values — 128 B, the byte
 // geometry of the f32 engine's K-tile, so the DMA and its swizzle are unchanged.
+//
+// X6 (dtype RDMI_F32_X6, round 5): three-way splits, x = x_hi + x_mid + x_lo + O(2^-26 |x|), and the six
+// products whose parts' orders sum to ≤ 2 (a_hi·w_hi, a_hi·w_mid, a_mid·w_hi, a_mid·w_mid, a_lo·w_hi,
+// a_hi·w_lo): a few 2^-24 per product — f32's own product rounding, the reference's exact-fp32 Linear
+// precision — in six bf16 MFMAs per 32-deep K step (≈0.4 of the exact engine's matrix time).  The
+// weight rows hold, per K-tile, [32 hi | 32 mid | 32 lo | 32 zero] bf16 = 256 B: two 128-B LDS rows per
+// output channel (the same DMA geometry), and the tile is 64 × 128 so that two workgroups still share
+// a CU (2 slots × (64 + 2·128) rows × 128 B = 80 KiB).
 #include "common.h"
 
 namespace {
@@ -141,14 +149,17 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
 // X3: bf16-split products (header).
 // NS: LDS ring slots — 3 (96 KiB: one workgroup per CU, two K-tiles in flight) or 2 (64 KiB: two
 // workgroups per CU, one K-tile in flight; the co-resident workgroup covers the DMA latency).
-template <int MODE, bool X3, int NS>
+// NP: 1 exact f32 products, 2 bf16x3 (X3), 3 bf16x6 (X6).
+template <int MODE, int NP, int NS>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P p) {
-  constexpr int BM = 128, BN = 128, NW = 4, WTM = 64, WTN = 64;
+  constexpr bool X3 = NP == 2;
+  constexpr int BM = NP == 3 ? 64 : 128, BN = 128, NW = 4, WTM = BM / 2, WTN = 64;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int AV = BM / 8 / NW, BV = BN / 8 / NW;  // 1-KiB DMA instructions per wave per K-tile
+  constexpr int BH = NP == 3 ? 2 : 1;  // 128-B LDS rows per weight row and K-tile
+  constexpr int AV = BM / 8 / NW, BV = BH * BN / 8 / NW;  // 1-KiB DMA instructions per wave per K-tile
   constexpr int LPS = AV + BV;
-  constexpr int SLOT = (BM + BN) * BKF;  // floats
-  __shared__ __attribute__((aligned(16))) float lds[NS * SLOT];  // 96 / 64 KiB
+  constexpr int SLOT = (BM + BH * BN) * BKF;  // floats
+  __shared__ __attribute__((aligned(16))) float lds[NS * SLOT];  // 96 / 64 / 80 KiB
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -187,11 +198,12 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
       arow[i] = mm * (int)p.lda;
     }
   }
-  int brow[BV];
+  int brow[BV];  // LDS row q = (i·NW + wid)·8 + lrow holds weight row q / BH, 128-B half q % BH
 #pragma unroll
   for (int i = 0; i < BV; ++i) {
-    const int n = n0 + (i * NW + wid) * 8 + lrow;
-    brow[i] = n < p.N ? n * (int)p.ldw : -1;
+    const int q = (i * NW + wid) * 8 + lrow;
+    const int n = n0 + q / BH;
+    brow[i] = n < p.N ? n * (int)p.ldw + (q % BH) * BKF : -1;
   }
   int tap = 0, cv = chunk;
   if (MODE != 0) {
@@ -228,11 +240,12 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
         ++tap;
       }
     }
+    const int kw = NP == 3 ? ks * 2 * BKF + chunk * 4 : kk;  // X6: a K-tile of W is 2 × 128 B per row
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
-      // X3: a K-tile of W is 32 hi then 32 lo bf16, always whole (zero padded past K)
-      const bool ok = brow[i] >= 0 && (X3 || kok);
-      dma16f(rw_, ok ? (unsigned)(brow[i] + kk) * 4u : OOB, lb + (i * NW + wid) * 8 * BKF);
+      // X3 / X6: a K-tile of W is always whole (its split parts, zero padded past K)
+      const bool ok = brow[i] >= 0 && (NP > 1 || kok);
+      dma16f(rw_, ok ? (unsigned)(brow[i] + kw) * 4u : OOB, lb + (i * NW + wid) * 8 * BKF);
     }
   };
 
@@ -256,7 +269,43 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
     asm volatile("" ::: "memory");
     issue(kt + NS - 1, (kt + NS - 1) % NS);  // into the slot read last in K-tile kt-1
     const float* la = lds + (kt % NS) * SLOT + (wm * WTM) * BKF;
-    const float* lb = lds + (kt % NS) * SLOT + BM * BKF + (wn * WTN) * BKF;
+    const float* lb = lds + (kt % NS) * SLOT + BM * BKF + (wn * WTN) * BH * BKF;
+    if constexpr (NP == 3) {
+      // lane quarter fq holds k = 8fq .. 8fq+7: A as f32 chunks 2fq, 2fq+1 split three ways; W as bf16
+      // chunks fq (hi) and 4+fq (mid) of LDS row 2·row, chunk fq (lo) of row 2·row + 1
+      bf16x8 as[RM][3], bs[RN][3];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int row = i * 16 + fr;
+        const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ (row & 7)) << 2));
+        const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ (row & 7)) << 2));
+        unsigned h[4], m[4], l[4];
+        rdmi::split3_bf16x2(a0[0], a0[1], h[0], m[0], l[0]);
+        rdmi::split3_bf16x2(a0[2], a0[3], h[1], m[1], l[1]);
+        rdmi::split3_bf16x2(a1[0], a1[1], h[2], m[2], l[2]);
+        rdmi::split3_bf16x2(a1[2], a1[3], h[3], m[3], l[3]);
+        as[i][0] = __builtin_bit_cast(bf16x8, u32x4{h[0], h[1], h[2], h[3]});
+        as[i][1] = __builtin_bit_cast(bf16x8, u32x4{m[0], m[1], m[2], m[3]});
+        as[i][2] = __builtin_bit_cast(bf16x8, u32x4{l[0], l[1], l[2], l[3]});
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int q0 = 2 * (j * 16 + fr), q1 = q0 + 1;
+        bs[j][0] = *(const bf16x8*)(lb + q0 * BKF + ((fq ^ (q0 & 7)) << 2));
+        bs[j][1] = *(const bf16x8*)(lb + q0 * BKF + (((4 + fq) ^ (q0 & 7)) << 2));
+        bs[j][2] = *(const bf16x8*)(lb + q1 * BKF + ((fq ^ (q1 & 7)) << 2));
+      }
+      // (weight part, activation part), largest first
+      constexpr int wpart[6] = {0, 0, 1, 1, 0, 2}, apart[6] = {0, 1, 0, 1, 2, 0};
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int t = 0; t < 6; ++t)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bs[j][wpart[t]], as[i][apart[t]], acc[i][j], 0, 0, 0);
+      continue;
+    }
     if constexpr (X3) {
       // lane quarter fq holds k = 8fq .. 8fq+7 of its row in both operands (the bf16 16x16x32 layout):
       // A as f32 chunks 2fq, 2fq+1 (split here), W as bf16 chunks fq (hi) and 4+fq (lo)
@@ -321,24 +370,27 @@ bool vec_ok(const GemmF32P& p) {
   return ok;
 }
 
-int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode, bool x3) {
+int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode, int np) {
   const char* gm = getenv("RDMI_GEMM_GROUP");
   p.group_m = gm ? atoi(gm) : 8;
-  dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, 128), batch);
+  const bool x3 = np == 2;
+  dim3 g(rdmi::div_up(p.N, 128), rdmi::div_up(p.M, np == 3 ? 64 : 128), batch);
   // RDMI_F32_SLOTS (read per launch, A/B): unset / 2 = two workgroups per CU with a 2-slot ring (the
   // default: +30-40 % for the bf16-split products, +12-15 % exact, bitwise the same —
   // profiles/r03k_f32_slots_ab.log), 3 = one workgroup per CU with a 3-slot ring
   const char* se = getenv("RDMI_F32_SLOTS");
   const bool ns2 = !(se && se[0] == '3');
 #define RDMI_F32_LAUNCH(M)                                                                     \
-  if (x3 && ns2)                                                                               \
-    hipLaunchKernelGGL((gemm_f32_kernel<M, true, 2>), g, dim3(256), 0, s, p);                 \
+  if (np == 3)                                                                                 \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, 3, 2>), g, dim3(256), 0, s, p);                    \
+  else if (x3 && ns2)                                                                          \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, 2, 2>), g, dim3(256), 0, s, p);                    \
   else if (x3)                                                                                 \
-    hipLaunchKernelGGL((gemm_f32_kernel<M, true, 3>), g, dim3(256), 0, s, p);                 \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, 2, 3>), g, dim3(256), 0, s, p);                    \
   else if (ns2)                                                                                \
-    hipLaunchKernelGGL((gemm_f32_kernel<M, false, 2>), g, dim3(256), 0, s, p);                \
+    hipLaunchKernelGGL((gemm_f32_kernel<M, 1, 2>), g, dim3(256), 0, s, p);                    \
   else                                                                                         \
-    hipLaunchKernelGGL((gemm_f32_kernel<M, false, 3>), g, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_f32_kernel<M, 1, 3>), g, dim3(256), 0, s, p);
   if (mode == 2) {
     RDMI_F32_LAUNCH(2)
   } else if (mode == 1) {
@@ -347,7 +399,7 @@ int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode, bool x3) {
     RDMI_F32_LAUNCH(0)
   }
 #undef RDMI_F32_LAUNCH
-  return rdmi::check_launch(x3 ? "gemm_f32x3" : "gemm_f32");
+  return rdmi::check_launch(np == 3 ? "gemm_f32x6" : x3 ? "gemm_f32x3" : "gemm_f32");
 }
 
 }  // namespace
@@ -355,12 +407,14 @@ int launch_f32(GemmF32P p, int batch, hipStream_t s, int mode, bool x3) {
 namespace rdmi {
 
 int gemm_f32(const rdmi_gemm_args* a, void* stream) {
-  const bool x3 = a->dtype == RDMI_F32_X3;
-  // X3: W is the bf16 split layout, ldw in bf16 elements (2 per f32 K position)
+  const int np = a->dtype == RDMI_F32_X6 ? 3 : a->dtype == RDMI_F32_X3 ? 2 : 1;
+  const bool x3 = np > 1;
+  // X3 / X6: W is the bf16 split layout, ldw in bf16 elements (2 / 4 per f32 K position)
   const long ldw = x3 ? a->ldw / 2 : a->ldw;
-  RDMI_REQUIRE(!x3 || (a->ldw % 64 == 0), RDMI_E_ALIGN, "gemm f32x3: ldw (%ld bf16) must be a multiple of 64", a->ldw);
+  RDMI_REQUIRE(!x3 || (a->ldw % 64 == 0), RDMI_E_ALIGN, "gemm f32x3/x6: ldw (%ld bf16) must be a multiple of 64", a->ldw);
   const int Kt = (a->K + BKF - 1) / BKF * BKF;
-  RDMI_REQUIRE(a->K % 4 == 0 && a->lda % 4 == 0 && ldw % 4 == 0 && ldw >= (x3 ? Kt : a->K), RDMI_E_ALIGN,
+  const long kw = np == 3 ? 2L * Kt : x3 ? Kt : a->K;  // floats of a weight row that the K-tiles read
+  RDMI_REQUIRE(a->K % 4 == 0 && a->lda % 4 == 0 && ldw % 4 == 0 && ldw >= kw, RDMI_E_ALIGN,
                "gemm f32: K (%d), lda (%ld), ldw (%ld) must be multiples of 4 (ldw >= K)", a->K, a->lda, ldw);
   RDMI_REQUIRE(al16(a->A) && al16(a->W) && a->strideA % 4 == 0 && a->strideW % 4 == 0, RDMI_E_ALIGN,
                "gemm f32: A/W not 16-byte aligned");
@@ -382,12 +436,14 @@ int gemm_f32(const rdmi_gemm_args* a, void* stream) {
   p.vec = vec_ok(p);
   RDMI_REQUIRE(!p.geglu || p.vec, RDMI_E_ALIGN, "gemm f32: GEGLU output needs 4-element aligned rows");
   p.a_bytes = (unsigned)(((long)(a->M - 1) * a->lda + a->K) * 4);
-  p.w_bytes = (unsigned)(((long)(a->N - 1) * ldw + (x3 ? Kt : a->K)) * 4);
-  return launch_f32(p, a->batch, (hipStream_t)stream, 0, x3);
+  p.w_bytes = (unsigned)(((long)(a->N - 1) * ldw + kw) * 4);
+  return launch_f32(p, a->batch, (hipStream_t)stream, 0, np);
 }
 
 int conv2d_f32(const rdmi_conv_args* a, void* stream) {
-  const bool x3 = a->dtype == RDMI_F32_X3;  // Kp counts f32 K positions (the bf16 rows are 2·Kp long)
+  // Kp counts f32 K positions (the bf16 rows are 2·Kp long for X3, 4·Kp for X6)
+  const int np = a->dtype == RDMI_F32_X6 ? 3 : a->dtype == RDMI_F32_X3 ? 2 : 1;
+  const bool x3 = np > 1;
   RDMI_REQUIRE(a->Cin % 4 == 0, RDMI_E_ALIGN, "conv2d f32: Cin (%d) must be a multiple of 4", a->Cin);
   const int K = a->kh * a->kw * a->Cin;
   RDMI_REQUIRE(a->Kp >= K && a->Kp % (x3 ? 32 : 4) == 0, RDMI_E_ARG, "conv2d f32: Kp (%d) must be >= %d, a multiple of %d",
@@ -398,7 +454,7 @@ int conv2d_f32(const rdmi_conv_args* a, void* stream) {
   RDMI_REQUIRE(!a->in_mean_rstd, RDMI_E_UNSUPPORTED, "conv2d f32: no fused input GroupNorm");
   RDMI_REQUIRE(!a->gn_part, RDMI_E_UNSUPPORTED, "conv2d f32: no GroupNorm moments");
   GemmF32P p{};
-  p.A = (const float*)a->x; p.Wt = (const float*)a->w; p.ldw = a->Kp;
+  p.A = (const float*)a->x; p.Wt = (const float*)a->w; p.ldw = np == 3 ? 2L * a->Kp : a->Kp;
   p.C = (float*)a->y; p.ldc = a->y_ld > 0 ? a->y_ld : a->Cout;
   p.bias = a->bias; p.R = (const float*)a->residual; p.ldr = a->res_ld > 0 ? a->res_ld : a->Cout;
   p.rowbias = a->rowbias; p.rpg = a->Ho * a->Wo; p.rb_ld = a->rowbias_ld;
@@ -413,8 +469,8 @@ int conv2d_f32(const rdmi_conv_args* a, void* stream) {
   RDMI_REQUIRE(!a->upsample || a->stride == 1, RDMI_E_UNSUPPORTED, "conv2d f32: upsample needs stride 1");
   p.vec = vec_ok(p);
   p.a_bytes = (unsigned)((long)a->B * a->H * a->W * a->Cin * 4);
-  p.w_bytes = (unsigned)((long)a->Cout * a->Kp * 4);
-  return launch_f32(p, 1, (hipStream_t)stream, dense ? 0 : (a->upsample ? 2 : 1), x3);
+  p.w_bytes = (unsigned)((long)a->Cout * p.ldw * 4);
+  return launch_f32(p, 1, (hipStream_t)stream, dense ? 0 : (a->upsample ? 2 : 1), np);
 }
 
 }  // namespace rdmi

@@ -95,9 +95,10 @@ BF16 = torch.bfloat16
 
 def _f32_x3_mode() -> str:
     m = os.environ.get("RDMI_F32_X3", "conv")
-    if m not in ("0", "1", "conv"):
+    if m not in ("0", "1", "conv", "6"):
         raise ValueError(f"RDMI_F32_X3={m!r}: 0 (exact f32 products everywhere), conv (default: bf16-split "
-                         f"products in the convolutions only) or 1 (bf16-split products everywhere)")
+                         f"products in the convolutions only), 1 (bf16-split products everywhere) or 6 "
+                         f"(f32-equivalent three-way bf16 split everywhere)")
     return m
 
 
@@ -118,20 +119,32 @@ def f32_x3(kind: str = "conv") -> bool:
 
 
 def f32_x6() -> bool:
-    """Whether the f32 path's cross-frame attention (with RDMI_F32_X3=conv) runs its products on the
-    three-way bf16 split (RDMI_F32_X6, rdmi.h: six bf16 MFMA products per f32 multiply-add, a few 2^-24
-    per product — f32's own product rounding) instead of the exact f32-input MFMA: the same precision
-    class at ≈2.5× the matrix rate.  RDMI_F32_X6=0 keeps the exact engine.  Read per attention call."""
-    return _f32_x3_mode() == "conv" and os.environ.get("RDMI_F32_X6", "1") != "0"
+    """Whether the f32 path's Linear layers and cross-frame attention (with RDMI_F32_X3=conv) run their
+    products on the three-way bf16 split (RDMI_F32_X6, rdmi.h: six bf16 MFMA products per f32
+    multiply-add, a few 2^-24 per product — f32's own product rounding) instead of the exact
+    f32-input MFMA: the same precision class at ≈2× the speed.  RDMI_F32_X6=0 keeps the exact engine.
+    Read when weights are packed, and per attention call."""
+    m = _f32_x3_mode()
+    return m == "6" or (m == "conv" and os.environ.get("RDMI_F32_X6", "1") != "0")
+
+
+def _f32_parts(kind: str) -> int:
+    """bf16 parts per f32 operand for `kind` ("conv" | "linear"): 1 exact f32, 2 bf16x3, 3 bf16x6."""
+    if f32_x3(kind):
+        return 2
+    if _f32_x3_mode() == "6":
+        return 3
+    return 3 if kind == "linear" and f32_x6() else 1
 
 
 def f32_precision_label() -> str:
     """The f32 path's product precision, for bench lines."""
     m = _f32_x3_mode()
     if m == "conv":
-        return "bf16x3 conv products, exact f32 Linear, " + \
-            ("f32-equivalent bf16x6 attention products" if f32_x6() else "exact f32 attention")
-    return {"0": "exact f32 products", "1": "bf16x3 products"}[m]
+        return "bf16x3 conv products, " + \
+            ("f32-equivalent bf16x6 Linear/attention products" if f32_x6() else "exact f32 Linear/attention")
+    return {"0": "exact f32 products", "1": "bf16x3 products",
+            "6": "f32-equivalent bf16x6 products everywhere"}[m]
 
 
 def split_bf16(w: torch.Tensor) -> torch.Tensor:
@@ -145,14 +158,40 @@ def split_bf16(w: torch.Tensor) -> torch.Tensor:
     return torch.stack((hi.view(n, kp // 32, 32), lo.view(n, kp // 32, 32)), 2).reshape(n, 2 * kp).contiguous()
 
 
+def split3_bf16(w: torch.Tensor) -> torch.Tensor:
+    """f32 [N, Kp] (Kp % 32 == 0) → bf16 [N, 4·Kp]: per 32-deep K-tile, bf16 hi, mid, lo parts then 32
+    zeros (each remainder exact in f32, each part round-to-nearest-even; the RDMI_F32_X6 weight layout
+    of rdmi.h, 256 B per row and K-tile).  The result carries `_rdmi_parts = 3`."""
+    n, kp = w.shape
+    if kp % 32:
+        raise ValueError(f"split3_bf16: K {kp} not a multiple of 32")
+    hi = w.to(BF16)
+    r = w - hi.float()
+    mid = r.to(BF16)
+    lo = (r - mid.float()).to(BF16)
+    z = torch.zeros_like(hi)
+    out = torch.stack([t.view(n, kp // 32, 32) for t in (hi, mid, lo, z)], 2).reshape(n, 4 * kp).contiguous()
+    out._rdmi_parts = 3
+    return out
+
+
+def _split_f32_weights(out: torch.Tensor, parts: int) -> torch.Tensor:
+    if parts == 2:
+        return split_bf16(out)
+    if parts == 3:
+        return split3_bf16(out)
+    return out
+
+
 def pack_linear(w: torch.Tensor, device, dtype=F16) -> torch.Tensor:
-    """[N, K] → [N, Kp] in the storage dtype (K zero-padded to a multiple of 32); f32 with
-    f32_x3(): split_bf16 of that ([N, 2·Kp] bf16)."""
+    """[N, K] → [N, Kp] in the storage dtype (K zero-padded to a multiple of 32); f32 with bf16-split
+    products for Linear layers (_f32_parts("linear")): split_bf16 ([N, 2·Kp] bf16) or split3_bf16
+    ([N, 4·Kp] bf16) of that."""
     n, k = w.shape
     kp = (k + 31) // 32 * 32
     out = torch.zeros((n, kp), dtype=dtype, device=device)
     out[:, :k] = w.to(device=device, dtype=dtype)
-    return split_bf16(out) if dtype == F32 and f32_x3("linear") else out
+    return _split_f32_weights(out, _f32_parts("linear")) if dtype == F32 else out
 
 
 def _w_code(a: torch.Tensor, w: torch.Tensor, name: str) -> int:
@@ -160,7 +199,7 @@ def _w_code(a: torch.Tensor, w: torch.Tensor, name: str) -> int:
     against split_bf16 weights."""
     if a.dtype == F32 and w.dtype == BF16:
         _need(w, BF16, name)
-        return _N.RDMI_F32_X3
+        return _N.RDMI_F32_X6 if getattr(w, "_rdmi_parts", 2) == 3 else _N.RDMI_F32_X3
     _need(w, a.dtype, name)
     return _N.RDMI_F32 if a.dtype == F32 else _N.RDMI_F16
 
@@ -198,8 +237,12 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16)
     kp = (k + 31) // 32 * 32
     out = torch.zeros((co, kp), dtype=dtype)
     out[:, :k] = t.reshape(co, k).to(dtype)
-    if dtype == F32 and f32_x3("conv"):
-        out = split_bf16(out)
+    if dtype == F32:
+        parts = _f32_parts("conv")
+        out = _split_f32_weights(out, parts).to(device)
+        if parts == 3:
+            out._rdmi_parts = 3
+        return out
     return out.to(device)
 
 
@@ -292,7 +335,8 @@ def gn_view(t: torch.Tensor, shape) -> torch.Tensor:
 
 
 def _engine_name(code: int) -> str:
-    return {_N.RDMI_F16: "implicit_gemm", _N.RDMI_F32: "implicit_gemm_f32", _N.RDMI_F32_X3: "implicit_gemm_f32x3"}[code]
+    return {_N.RDMI_F16: "implicit_gemm", _N.RDMI_F32: "implicit_gemm_f32", _N.RDMI_F32_X3: "implicit_gemm_f32x3",
+            _N.RDMI_F32_X6: "implicit_gemm_f32x6"}[code]
 
 
 def _gemm_args(a, w, out, bias, residual, rowbias, rpg, alpha, M, Nn, K, batch, geglu, out_f32):
@@ -393,7 +437,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
                    out[s0:s1], alpha, out_hw, in_gn=ig, _gn_slot=slot, w_up2=w_up2)
         _gn_attach(out, part)
         return out
-    kp = w.shape[1] // 2 if code == _N.RDMI_F32_X3 else w.shape[1]
+    kp = w.shape[1] // {_N.RDMI_F32_X3: 2, _N.RDMI_F32_X6: 4}.get(code, 1)
     if kp < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {kp} < {k * k * Cin}")
     if w_up2 is not None and (f32 or os.environ.get("RDMI_UP2", "0") != "1"):
