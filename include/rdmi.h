@@ -123,11 +123,16 @@ typedef struct rdmi_conv_args {
   int dtype;
   /* Optional, upsample = 1 only: the same conv's weights for the phase-decomposed form — the ×2
    * nearest upsample + 3×3 conv computed as four 2×2 convs on the source grid, one per output
-   * phase (a, c) = (y & 1, x & 1), the 3×3 taps that read the same source pixel summed
-   * (rows {0 | 1,2} for a = 0, {0,1 | 2} for a = 1; columns likewise): 4/9 of the MFMA work.
-   * Layout [4 phases (2a + c)][Cout][Cin/64][2][2][64] f16 (row stride 4·Cin).  Used where the
-   * 256-channel halo engine runs the conv (f16, Cout % 256 == 0, Cin % 64 == 0, Ho % 32 == 0,
-   * Wo % 32 == 0, no input GroupNorm); elsewhere `w` is used.  NULL: off. */
+   * phase (a, c) = (y & 1, x & 1), the 3×3 taps that read the same source pixel merged
+   * (rows {0 | 1,2} for a = 0, {0,1 | 2} for a = 1; columns likewise).  A merged weight Σw (sum in
+   * f32 of 2 or 4 f16 taps) is stored as hi = f16(Σw) and lo = f16(Σw − hi), so every product is
+   * exact in the f32 accumulator: the result is the 9-tap conv's up to f32 accumulation order (and
+   * lo's f16 rounding where Σw − hi is subnormal or wider than 11 bits), in 7/9 of the MFMA work.
+   * Layout [4 phases (2a + c)][Cout][Cin/64][7][64] f16 (row stride 7·Cin): per 64-channel block
+   * the hi parts of taps (dy, dx) = (0,0), (0,1), (1,0), (1,1), then the lo parts of those taps other
+   * than (a, c) (a single 3×3 weight, exact in f16), in the same order.  Used where the halo engine
+   * runs the conv (f16, Cin % 64 == 0, Ho % 32 == 0, Wo % 32 == 0, no input GroupNorm); elsewhere
+   * `w` is used.  NULL: off. */
   const void* w_up2;
   /* Optional with in_mean_rstd (round 5): the input GroupNorm's per-channel scale / shift as
    * rdmi_groupnorm_affine writes them, [B][Cin/64][2][64] f32 — per image and 64-channel block the 64

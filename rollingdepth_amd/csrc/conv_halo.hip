@@ -11,12 +11,10 @@ static void halo_gn(bool gn, dim3 g, hipStream_t s, const GemmP& p) {
     hipLaunchKernelGGL((conv_halo_kernel<MODE, NPH, WN, false>), g, dim3(512), 0, s, p);
 }
 
-// (mode, nph, wn): (3, 2, 4) phase-decomposed upsample (no GroupNorm input); (1|2, 2, 4) and
-// (1|2, 1, 2) with or without the GroupNorm input; (1|2, 4, 4) without
+// (mode, nph, wn): (1|2, 2, 4) and (1|2, 1, 2) with or without the GroupNorm input; (1|2, 4, 4)
+// without
 void launch_conv_halo(int mode, int nph, int wn, bool gn, dim3 g, hipStream_t s, const GemmP& p) {
-  if (mode == 3) {
-    hipLaunchKernelGGL((conv_halo_kernel<3, 2, 4, false>), g, dim3(512), 0, s, p);
-  } else if (wn == 2) {
+  if (wn == 2) {
     if (mode == 2)
       halo_gn<2, 1, 2>(gn, g, s, p);
     else

@@ -17,7 +17,12 @@ static void occ2_mode_launch(bool gn, bool pipe, dim3 g, hipStream_t s, const Ge
 }
 
 void launch_conv_occ2(int mode, bool gn, bool pipe, dim3 g, hipStream_t s, const GemmP& p) {
-  if (mode == 2)
+  if (mode == 3) {  // phase-decomposed upsample (no GroupNorm input)
+    if (pipe)
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<3, false, true>), g, dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((conv_halo_occ2_kernel<3, false, false>), g, dim3(256), 0, s, p);
+  } else if (mode == 2)
     occ2_mode_launch<2>(gn, pipe, g, s, p);
   else
     occ2_mode_launch<1>(gn, pipe, g, s, p);

@@ -268,11 +268,11 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     const unsigned patches = (unsigned)((a->Ho / 16) * (a->Wo / 16) * a->B);
     const bool gn = p.gmr != nullptr;
-    if (a->upsample && a->w_up2 && !gn && a->Cout % 256 == 0 && a->Ho % 32 == 0 && a->Wo % 32 == 0 &&
-        al16(a->w_up2)) {  // phase-decomposed ×2 upsample conv (4 taps per phase)
-      p.Wt = (const f16*)a->w_up2; p.ldw = 4L * a->Cin; p.K = p.Kvalid = 4 * a->Cin;
+    if (a->upsample && a->w_up2 && !gn && a->Ho % 32 == 0 && a->Wo % 32 == 0 && al16(a->w_up2)) {
+      // phase-decomposed ×2 upsample conv: 4 hi + 3 lo taps per phase (conv_halo_occ2_kernel MODE 3)
+      p.Wt = (const f16*)a->w_up2; p.ldw = 7L * a->Cin; p.K = p.Kvalid = 7 * a->Cin;
       p.w_bytes = (unsigned)(4L * a->Cout * p.ldw * 2);
-      launch_conv_halo(3, 2, 4, false, dim3(a->Cout / 256, patches, 1), st, p);
+      launch_conv_occ2(3, false, p.conv_pipe != 0, dim3((a->Cout + 127) / 128, patches, 1), st, p);
     } else if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256 || p.gaff))) {
       dim3 g(a->Cout / 256, patches, 1);
       const bool ph2 = hmode != 1 || gn;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)

@@ -191,7 +191,7 @@ struct PatchRows {  // patch rows y0 + rw + i (i = fragment), columns x0 + fr; H
   __device__ int group(int, int rpg) const { return rpg == Ho * Wo ? b : -1; }  // conv: rpg = Ho·Wo
   __device__ int rstep() const { return Wo; }
 };
-// Output phase (a, c) of a ×2-upsampled conv computed on the source grid (conv_halo_kernel MODE 3):
+// Output phase (a, c) of a ×2-upsampled conv computed on the source grid (conv_halo_occ2_kernel MODE 3):
 // phase-grid patch rows y0 + rw + i, columns x0 + fr → output pixel (2y + a, 2x + c) of the
 // Ho × Wo output.  Moment slots: image b's range [b·HoWo/32, (b+1)·HoWo/32) split into the four
 // phases' sub-ranges of (Ho/2)(Wo/2)/32 slots, each laid out as PatchRows' on the phase grid.
@@ -1090,13 +1090,6 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmP p) {
 // ends with lgkmcnt(0); the last write (tap 8 phase 0) is ≥ 2 barriers before the first read of
 // block cb+1 by the group running one barrier ahead.  Halo pixels outside the image stay zero (the conv's zero padding is
 // applied after the norm).  Halo(0) is normalised in the prologue.
-// MODE 3: nearest ×2 upsample + 3×3 conv as four 2×2 convs on the source grid, one per output
-// phase (a, c) = (y & 1, x & 1) (the 3×3 taps that land on the same source pixel summed into one
-// weight: rows {0 | 1, 2} for a = 0, {0, 1 | 2} for a = 1, likewise columns; zero padding maps to
-// zero padding), 4/9 of MODE 2's MFMA work.  A tile is 16×16 pixels of one phase; its 17×17 source
-// halo (origin (y0 − 1 + a, x0 − 1 + c)) sits in the 18×18 halo buffer; weights p.Wt + phase·N·ldw
-// in the cmaj order with 4 taps (dy, dx) ∈ {0, 1}²; halo(cb+1) pieces 0-2 issued in tap 1, 3-5 in
-// tap 2, all landed by tap 3's wait.
 // STAMP = 1 (diagnostic build only, tools/conv_stamp.hip): per-wave cycle sums — 0 prologue, 1 load
 // sections (fragment reads, DMA issue, waits), 2 barrier before the MFMAs, 3 MFMA issue, 4 GroupNorm
 // transform, 5 barrier after, 6 epilogue, 7 total — written to p.stamps.
@@ -1111,7 +1104,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
     }
   };
   if constexpr (STAMP) st_start = st_prev = gk_stamp();
-  constexpr int NT = MODE == 3 ? 4 : 9;    // taps per channel block
+  constexpr int NT = 9;                    // taps per channel block
   constexpr int WM = 8 / WN;
   constexpr int BN = WN * 64, BKP = 64, RM = 16 / WM, RN = 4;
   constexpr int NRG = NPH == 4 ? 2 : NPH;  // row groups of a wave (one per phase group)
@@ -1127,7 +1120,6 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   constexpr int GNT = GN ? 1024 : 0;       // GroupNorm scale/shift table: sc[1024], sh[1024] floats
   static_assert(RPG == 4 && (NPH != 1 || WN == 2) && (WN != 2 || NPH == 1) && (!GN || NPH != 4),
                 "unsupported halo variant");
-  static_assert(MODE != 3 || (NPH == 2 && WN == 4 && !GN), "phase-decomposed upsample: NPH 2, WN 4, no GN");
   __shared__ __attribute__((aligned(16))) f16 lds[2 * HALO + NBS * BSLOT + 4 * GNT];
   float* const gnt = (float*)(lds + 2 * HALO + NBS * BSLOT);
 
@@ -1141,13 +1133,10 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   int mt_, nt_;
   tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
   const int n0 = nt_ * BN;
-  // MODE 3: m-tile = (image, phase, 16×16 tile of the Ho/2 × Wo/2 phase grid)
-  const int pxn = p.Wo >> (MODE == 3 ? 5 : 4), pyn = p.Ho >> (MODE == 3 ? 5 : 4);
+  const int pxn = p.Wo >> 4, pyn = p.Ho >> 4;
   const int px = mt_ % pxn;
   const int py = (mt_ / pxn) % pyn;
-  const int phs = MODE == 3 ? (mt_ / (pxn * pyn)) & 3 : 0;
-  const int b = mt_ / (pxn * pyn * (MODE == 3 ? 4 : 1));
-  const int pa = phs >> 1, pc = phs & 1;
+  const int b = mt_ / (pxn * pyn);
   const int y0 = py * 16, x0 = px * 16;
   const __amdgpu_buffer_rsrc_t ra_ =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
@@ -1163,7 +1152,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   for (int e = 0; e < HPW; ++e) {
     const int hp = (wid + 8 * e) * 8 + lrow;
     const int hr = hp / HWD, hc = hp - hr * HWD;
-    const int yy = y0 - 1 + pa + hr, xx = x0 - 1 + pc + hc;
+    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
     const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
     hvo[e] = ok ? (unsigned)(((b * p.IH + sy) * p.IW + sx) * p.Cin + chunk * 8) * 2u : OOB;
@@ -1173,7 +1162,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   for (int e = 0; e < NB; ++e) {
     const int rt = (wid + 8 * e) * 8 + lrow;  // LDS row of the tile
     const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
-    bvo[e] = n < p.N ? (unsigned)((phs * p.N + n) * (int)p.ldw + chunk * 8) * 2u : OOB;
+    bvo[e] = n < p.N ? (unsigned)(n * (int)p.ldw + chunk * 8) * 2u : OOB;
   }
   const int ncb = p.Cin >> 6;
   const int wids = __builtin_amdgcn_readfirstlane(wid);
@@ -1270,9 +1259,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   for (int u = 0; u < nk; ++u) {
     const int cb = u / NT;  // wave-uniform
     const int tap = u - cb * NT;
-    const int dy = MODE == 3 ? tap >> 1 : (tap * 11) >> 5, dx = MODE == 3 ? tap & 1 : tap - 3 * dy;
+    const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
     const f16* lb = lds + 2 * HALO + (u % NBS) * BSLOT + (wn * 64) * BKP;
-    const bool halo_now = MODE != 3 && tap >= 1 && tap <= HPW && hv(tap - 1);
+    const bool halo_now = tap >= 1 && tap <= HPW && hv(tap - 1);
     // halo pixel of fragment row r = RM·wm + 4·rg + i, lane fr: hp = (r + dy)·18 + dx + fr, whose
     // swizzle term hp & 7 = (fr + dx + 2(i + dy)) & 7 does not depend on wm or rg (RM·18, 72 ≡ 0 mod 8)
     const int xb = fr + dx + 2 * dy;
@@ -1315,26 +1304,6 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
           issueB(u + 2, 2, 4);
         }
         if (ph == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      } else if (NPH == 2 && MODE == 3) {
-        if (ph == 0) {
-          if (tap == 1) {
-#pragma unroll
-            for (int e = 0; e < 3; ++e) issueHalo(cb + 1, e);
-          } else if (tap == 2) {
-#pragma unroll
-            for (int e = 3; e < HPW; ++e)
-              if (hv(e)) issueHalo(cb + 1, e);
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // B(u) read for the last time
-        } else {
-          if (tap == 1)
-            wait_vmcnt<3>();  // B(u+1) landed (halo pieces 0-2 in flight)
-          else if (tap == 2)
-            wait_vmcnt<2>();  // B(u+1) and pieces 0-2 landed (3-4, and 5 on wave 0, in flight)
-          else
-            wait_vmcnt<0>();  // B(u+1) (and on tap 3 all of halo(cb+1)) landed
-          issueB(u + 2, 0, NB);
-        }
       } else if (NPH == 2) {
         if (ph == 0) {
           if (halo_now) issueHalo(cb + 1, tap - 1);
@@ -1391,11 +1360,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(GemmP p) {
   wait_vmcnt<0>();  // drain the trailing zero-chunk DMAs before the workgroup can retire
   seg(5);
 
-  if constexpr (MODE == 3)
-    store_tile<RM, RN, 64, true>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr, fq,
-                           p.cperm);
-  else
-    store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
+  store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq, p.cperm);
   if constexpr (STAMP) {
     wait_vmcnt<0>();
     seg(6);
@@ -1435,6 +1400,16 @@ __device__ __forceinline__ void occ2_sched(std::integer_sequence<int, S...>) {
 // fragment reads and 64 MFMAs.  At a channel block's first tap the halo is refilled in place:
 // barrier (all reads of the previous block's halo done), DMA, wait, [GroupNorm+SiLU of the own
 // pieces], barrier.
+// MODE 3: nearest ×2 upsample + 3×3 conv as four 2×2 convs on the source grid, one per output
+// phase (a, c) = (y & 1, x & 1): the 3×3 taps that land on the same source pixel (rows {0 | 1, 2}
+// for a = 0, {0, 1 | 2} for a = 1, columns likewise) act through one merged weight, stored as an
+// f16 hi + lo pair (hi = f16(Σ w), lo = f16(Σ w − hi), Σ in f32: rdmi.h rdmi_conv_args.w_up2), so
+// each product x·hi, x·lo is exact in the f32 accumulator and the result is the 9-tap conv's up to
+// f32 accumulation order.  Per 64-channel block 7 K-tiles: the 4 hi taps (dy, dx) ∈ {0, 1}², then
+// the lo parts of the 3 taps that merge 2 or 4 weights (the phase's single-weight tap (a, c) is
+// exact in f16 and has no lo part) — 7/9 of MODE 2's MFMA work.  A tile is 16×16 pixels of one
+// phase grid (Ho/2 × Wo/2); its 17×17 source halo (origin (y0 − 1 + a, x0 − 1 + c)) sits in the
+// 18×18 halo buffer; weights p.Wt + phase·N·ldw.
 // STAMP = 1 (diagnostic build only, tools/conv_stamp.hip): per-wave cycle sums of the segments —
 // 0 prologue, 1 K-tile wait + barrier, 2 fragment reads + MFMA issue, 3 halo refill (barrier, DMA,
 // wait, GroupNorm transform, barrier), 4 epilogue, 5 total — written to p.stamps.
@@ -1470,10 +1445,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   int mt_, nt_;
   tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
   const int n0 = nt_ * BN;
-  const int pxn = p.Wo >> 4, pyn = p.Ho >> 4;
+  constexpr int NT = MODE == 3 ? 7 : 9;  // K-tiles (taps) per channel block
+  // MODE 3: m-tile = (image, phase, 16×16 tile of the Ho/2 × Wo/2 phase grid)
+  const int pxn = p.Wo >> (MODE == 3 ? 5 : 4), pyn = p.Ho >> (MODE == 3 ? 5 : 4);
   const int px = mt_ % pxn;
   const int py = (mt_ / pxn) % pyn;
-  const int b = mt_ / (pxn * pyn);
+  const int phs = MODE == 3 ? (mt_ / (pxn * pyn)) & 3 : 0;
+  const int b = mt_ / (pxn * pyn * (MODE == 3 ? 4 : 1));
+  const int pa = phs >> 1, pc = phs & 1;
   const int y0 = py * 16, x0 = px * 16;
   const __amdgpu_buffer_rsrc_t ra_ =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
@@ -1488,7 +1467,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   for (int e = 0; e < HPW; ++e) {
     const int hp = (wid + 4 * e) * 8 + lrow;
     const int hr = hp / HWD, hc = hp - hr * HWD;
-    const int yy = y0 - 1 + hr, xx = x0 - 1 + hc;
+    const int yy = y0 - 1 + pa + hr, xx = x0 - 1 + pc + hc;
     const bool ok = hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
     hvo[e] = ok ? (unsigned)(((b * p.IH + sy) * p.IW + sx) * p.Cin + chunk * 8) * 2u : OOB;
@@ -1498,7 +1477,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   for (int e = 0; e < NB; ++e) {
     const int rt = (wid + 4 * e) * 8 + lrow;  // LDS row of the tile
     const int n = n0 + (p.cperm ? (rt & ~63) + perm64(rt & 63) : rt);
-    bvo[e] = n < p.N ? (unsigned)(n * (int)p.ldw + chunk * 8) * 2u : OOB;
+    bvo[e] = n < p.N ? (unsigned)((phs * p.N + n) * (int)p.ldw + chunk * 8) * 2u : OOB;
   }
   const int ncb = p.Cin >> 6;
   auto hv = [&](int e) { return wids + 4 * e < HPC; };
@@ -1561,7 +1540,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = ncb * 9;
+  const int nk = ncb * NT;
   const int fr = lane & 15, fq = lane >> 4;
   const int off0 = fr * BKP + ((fq ^ (fr & 7)) << 3);
   const int off1 = fr * BKP + (((4 + fq) ^ (fr & 7)) << 3);
@@ -1597,9 +1576,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   const bool live = n0 + (wids & 1) * 64 < p.N;  // wave-uniform
   seg(0);
   for (int u = 0; u < nk; ++u) {
-    const int cb = u / 9;
-    const int tap = u - cb * 9;
-    const int dy = (tap * 11) >> 5, dx = tap - 3 * dy;
+    const int cb = u / NT;
+    const int tap = u - cb * NT;
+    // MODE 3: K-tiles 0-3 the hi parts of taps t = 2dy + dx, 4-6 the lo parts of the taps t ≠ phase
+    const int t4 = tap < 4 ? tap : tap - 4 + (tap - 4 >= phs ? 1 : 0);
+    const int dy = MODE == 3 ? t4 >> 1 : (tap * 11) >> 5, dx = MODE == 3 ? t4 & 1 : tap - 3 * dy;
     if (u > 0) seg(2);
     if (u > 0) {
       if (tap == 0) {  // refill the halo with channel block cb
@@ -1684,9 +1665,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     }
   }
   seg(2);
-  if (live)
-    store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq,
-                                 p.cperm);
+  if (live) {
+    if constexpr (MODE == 3)
+      store_tile<RM, RN, 64, true>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr,
+                                   fq, p.cperm);
+    else
+      store_tile<RM, RN, 64, true>(p, acc, PatchRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr}, n0 + wn * 64, 0, fr, fq,
+                                   p.cperm);
+  }
   if constexpr (STAMP) {
     wait_vmcnt<0>();
     seg(4);

@@ -248,26 +248,35 @@ def pack_conv(w: torch.Tensor, device, cin_pad: Optional[int] = None, dtype=F16)
 
 def pack_conv_up2(w: torch.Tensor, device, cin_pad: Optional[int] = None) -> Optional[torch.Tensor]:
     """3×3 weights [Cout, Cin, 3, 3] of a conv behind a nearest ×2 upsample → the four output
-    phases' 2×2 weights (rdmi.h rdmi_conv_args.w_up2): [4 (2a + c), Cout, 4·Cin_pad] f16 in the
-    order [Cin_pad/64][dy][dx][64].  Phase a reads source rows (i − 1 + a, i + a): 3×3 rows {0}, {1, 2}
-    for a = 0 and {0, 1}, {2} for a = 1 land on them (columns likewise), so their weights are
-    summed — in f32 from the checkpoint's values, rounded to f16 once.  None when Cin_pad % 64."""
+    phases' merged 2×2 weights as f16 hi / lo pairs (rdmi.h rdmi_conv_args.w_up2): [4 (2a + c), Cout,
+    7·Cin_pad] f16 in the order [Cin_pad/64][7][64] — the hi parts of taps (dy, dx) = (0,0), (0,1),
+    (1,0), (1,1), then the lo parts of the three taps other than (a, c).  Phase a reads source rows
+    (i − 1 + a, i + a): 3×3 rows {0}, {1, 2} for a = 0 and {0, 1}, {2} for a = 1 land on them
+    (columns likewise), so their weights are summed — in f32 from the f16-rounded weights the 9-tap
+    conv multiplies by (exact: ≤ 4 f16 values) — and split hi = f16(Σ), lo = f16(Σ − hi).  Tap (a, c)
+    is a single 3×3 weight (lo = 0, not stored).  None when Cin_pad % 64."""
     co, ci, kh, kw = w.shape
     cp = cin_pad or pad_channels(ci)
     if (kh, kw) != (3, 3) or cp % 64:
         return None
     sets = (((0,), (1, 2)), ((0, 1), (2,)))
-    wf = w.float()
-    out = torch.zeros((4, co, cp // 64, 2, 2, 64), dtype=F32)
+    wf = w.to(F16).float()  # the values pack_conv stores
+    out = torch.zeros((4, co, cp // 64, 7, 64), dtype=F16)
     for a in range(2):
         for c in range(2):
-            for dy in range(2):
-                for dx in range(2):
-                    t = sum(wf[:, :, ky, kx] for ky in sets[a][dy] for kx in sets[c][dx])  # [Cout, Cin]
-                    tp = torch.zeros((co, cp), dtype=F32)
-                    tp[:, :ci] = t
-                    out[2 * a + c, :, :, dy, dx, :] = tp.reshape(co, cp // 64, 64)
-    return out.reshape(4, co, 4 * cp).to(F16).to(device)
+            ph = 2 * a + c
+            lo_slot = 4
+            for t in range(4):
+                dy, dx = t >> 1, t & 1
+                sm = sum(wf[:, :, ky, kx] for ky in sets[a][dy] for kx in sets[c][dx])  # [Cout, Cin], exact
+                tp = torch.zeros((co, cp), dtype=F32)
+                tp[:, :ci] = sm
+                hi = tp.to(F16)
+                out[ph, :, :, t, :] = hi.reshape(co, cp // 64, 64)
+                if t != ph:
+                    out[ph, :, :, lo_slot, :] = (tp - hi.float()).to(F16).reshape(co, cp // 64, 64)
+                    lo_slot += 1
+    return out.reshape(4, co, 7 * cp).to(device)
 
 
 # ----------------------------------------------------------------------------- GEMM / conv
@@ -441,11 +450,11 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     if kp < k * k * Cin:
         raise ValueError(f"conv2d: packed weight K {kp} < {k * k * Cin}")
     if w_up2 is not None and (f32 or os.environ.get("RDMI_UP2", "0") != "1"):
-        w_up2 = None  # opt-in: see DESIGN.md §7 (same accuracy in expectation, but the 768² depth
-        # parity sits on the min/max renormalisation of two pixels — tools/depth_sensitivity.py)
-    if w_up2 is not None and (w_up2.dtype != F16 or tuple(w_up2.shape) != (4, cout, 4 * Cin) or
+        w_up2 = None  # opt-in (RDMI_UP2=1): DESIGN.md §4 — the phase form moves 0.2 % of the outputs
+        # by 1 ulp, and any such change re-draws the depth error's extreme-pixel offset
+    if w_up2 is not None and (w_up2.dtype != F16 or tuple(w_up2.shape) != (4, cout, 7 * Cin) or
                               not w_up2.is_contiguous()):
-        raise ValueError(f"conv2d: w_up2 must be pack_conv_up2's [4, {cout}, {4 * Cin}] f16")
+        raise ValueError(f"conv2d: w_up2 must be pack_conv_up2's [4, {cout}, {7 * Cin}] f16")
     a = _conv_args(x, w, cout, k, stride, pad, pad_tl, upsample, bias, residual, rowbias, out, alpha, Ho, Wo, in_gn,
                    w_up2)
     a.dtype = code
@@ -466,10 +475,11 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     elif _gn_slot is not None:
         a.gn_part, a.gn_ld = _gn_slot
     es = x.element_size()
-    # executed MFMA work: 4 taps per output pixel where the phase-decomposed upsample runs (whose
-    # weights are the 4 phases × 4 taps)
-    taps = 4 if (w_up2 is not None and _up2_runs(a)) else k * k
-    nb = es * (x.numel() + cout * (16 if taps == 4 else k * k) * Cin +
+    # executed MFMA work: 7 taps per output pixel where the phase-decomposed upsample runs (whose
+    # weights are the 4 phases × 7 taps)
+    up2 = w_up2 is not None and _up2_runs(a)
+    taps = 7 if up2 else k * k
+    nb = es * (x.numel() + cout * (28 if up2 else k * k) * Cin +
                (2 if residual is not None else 1) * B * Ho * Wo * cout)
     with _Timed(_engine_name(code), 2.0 * B * Ho * Wo * cout * taps * Cin,
                 f"conv{k} B={B} {Ho}x{Wo} {Cin}->{cout} s{stride}{' up' if upsample else ''}{' gn' if in_gn else ''}",
@@ -483,7 +493,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
 def _up2_runs(a) -> bool:
     """Mirror of rdmi_conv2d's choice of the phase-decomposed upsample form (gemm.hip)."""
     hm = int(os.environ.get("RDMI_CONV_HALO", "3"))
-    return (a.upsample == 1 and bool(a.w_up2) and not a.in_mean_rstd and a.Cout % 256 == 0 and a.Ho % 32 == 0 and
+    return (a.upsample == 1 and bool(a.w_up2) and not a.in_mean_rstd and a.Ho % 32 == 0 and
             a.Wo % 32 == 0 and hm != 0 and a.kh == 3 and a.kw == 3 and a.Cin % 64 == 0 and a.stride == 1 and
             a.pad_top == 1 and a.pad_left == 1 and a.Ho == 2 * a.H and a.Wo == 2 * a.W)
 

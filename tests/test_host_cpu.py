@@ -90,30 +90,42 @@ def test_split_bf16_layout(monkeypatch):
 
 
 def test_pack_conv_up2_phase_identity():
-    """pack_conv_up2: conv3×3(nearest×2(x)) == the four 2×2 phase convs on the source grid
-    (rdmi.h rdmi_conv_args.w_up2) — the identity the GPU's phase-decomposed upsample relies on,
-    checked in f64 on the packed weights' f16 values (and the phase tensor's layout)."""
+    """pack_conv_up2: conv3×3(nearest×2(x)) == the four 2×2 phase convs on the source grid with
+    merged weights hi + lo (rdmi.h rdmi_conv_args.w_up2) — the identity the GPU's phase-decomposed
+    upsample relies on, checked in f64 against the 9-tap conv of the f16-rounded weights (what the
+    9-tap kernel multiplies by), and the [phase][Cout][Cin/64][7][64] layout."""
     from rollingdepth_amd import kernels as K
 
     torch.manual_seed(0)
     B, Cin, Cout, H, W = 2, 128, 8, 5, 7
     x = torch.randn(B, Cin, H, W, dtype=torch.float64)
-    w = torch.randn(Cout, Cin, 3, 3)
+    w = torch.randn(Cout, Cin, 3, 3) * 0.05
     wu = K.pack_conv_up2(w, "cpu")
-    assert wu.shape == (4, Cout, 4 * Cin) and wu.dtype == torch.float16
-    wph = wu.double().view(4, Cout, Cin // 64, 2, 2, 64).permute(0, 1, 2, 5, 3, 4).reshape(4, Cout, Cin, 2, 2)
+    assert wu.shape == (4, Cout, 7 * Cin) and wu.dtype == torch.float16
+    t7 = wu.double().view(4, Cout, Cin // 64, 7, 64)
+    wph = torch.zeros(4, Cout, Cin // 64, 4, 64, dtype=torch.float64)
+    for ph in range(4):
+        wph[ph] = t7[ph, :, :, :4]
+        lo_taps = [t for t in range(4) if t != ph]  # lo parts in tap order, the phase's own tap has none
+        for s_, t in enumerate(lo_taps):
+            wph[ph, :, :, t] += t7[ph, :, :, 4 + s_]
+    wph = wph.view(4, Cout, Cin // 64, 2, 2, 64).permute(0, 1, 2, 5, 3, 4).reshape(4, Cout, Cin, 2, 2)
+    w16 = w.half().double()
     ref = torch.nn.functional.conv2d(torch.nn.functional.interpolate(x, scale_factor=2.0, mode="nearest"),
-                                     w.double(), padding=1)
+                                     w16, padding=1)
     xp = torch.nn.functional.pad(x, (1, 1, 1, 1))
     got = torch.empty_like(ref)
     for a in range(2):
         for c in range(2):
             got[:, :, a::2, c::2] = torch.nn.functional.conv2d(xp[:, :, a:a + H + 1, c:c + W + 1], wph[2 * a + c])
-    # f16 rounding of the summed weights only
-    assert (got - ref).abs().max().item() < 2e-3 * ref.abs().max().item()
-    exact = wu.double().view(4, Cout, Cin // 64, 2, 2, 64)
-    assert torch.equal(exact[0, :, :, 1, 1], (w[:, :, 1:, 1:].sum((2, 3))).half().double().view(Cout, 2, 64))
-    assert torch.equal(exact[3, :, :, 0, 0], (w[:, :, :2, :2].sum((2, 3))).half().double().view(Cout, 2, 64))
+    # hi + lo carries each merged weight to within lo's own f16 rounding (≤ 2^-22 of it here)
+    assert (got - ref).abs().max().item() < 1e-6 * ref.abs().max().item()
+    # the phase's single-weight tap is the f16 weight itself; a 4-weight tap is hi + lo of the exact sum
+    assert torch.equal(t7[0, :, :, 0], w16[:, :, 0, 0].reshape(Cout, 2, 64))
+    s4 = w16[:, :, 1:, 1:].sum((2, 3))
+    assert torch.equal(t7[0, :, :, 3], s4.half().double().reshape(Cout, 2, 64))
+    assert torch.equal(t7[0, :, :, 6], (s4 - s4.half().double()).half().double().reshape(Cout, 2, 64))
+    assert torch.equal(t7[3, :, :, 3], w16[:, :, 2, 2].reshape(Cout, 2, 64))
     assert K.pack_conv_up2(torch.randn(4, 32, 3, 3), "cpu") is None  # Cin_pad % 64 != 0
 
 

@@ -193,12 +193,16 @@ def test_groupnorm_moments_from_conv(B, H, W, Cin, Cout, up, engine, h32):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,res", [(2, 16, 16, 256, 256, False), (1, 32, 48, 512, 512, False),
                                                  (3, 16, 32, 128, 256, True), (1, 48, 16, 64, 512, True),
-                                                 (2, 8, 24, 256, 256, False)])
+                                                 (2, 8, 24, 256, 256, False), (2, 16, 16, 128, 128, True),
+                                                 (1, 16, 32, 64, 320, False)])
 def test_conv2d_up2_phases(B, H, W, Cin, Cout, res, monkeypatch):
-    """Upsample2D's nearest ×2 + 3×3 conv as four 2×2 phase convs on the source grid
-    (rdmi_conv_args.w_up2, conv_halo_kernel MODE 3) against the fp32 conv of the upsampled input,
-    against the 9-tap form, with the epilogue's GroupNorm moments and per-image batch invariance.
-    (2, 8, 24): Ho = 16 is not a phase-tile multiple — the 9-tap form runs (bitwise check)."""
+    """Upsample2D's nearest ×2 + 3×3 conv as four 2×2 phase convs on the source grid with hi + lo
+    merged weights (rdmi_conv_args.w_up2, conv_halo_occ2_kernel MODE 3, RDMI_UP2=1) against the
+    9-tap form: the same products, so the f16 outputs differ only where the f32 accumulation order
+    moves a value across an f16 rounding boundary — at most 1 ulp, on a small fraction of the
+    outputs; also against the fp32 conv, with the epilogue's GroupNorm moments and per-image batch
+    invariance.  (2, 8, 24): Ho = 16 is not a phase-tile multiple — the 9-tap form runs (bitwise).
+    Cout 128 / 320: 128-channel tiles, the last one ragged."""
     K_ = _k()
     monkeypatch.setenv("RDMI_UP2", "1")
     g = torch.Generator(device=DEV).manual_seed(13)
@@ -209,7 +213,7 @@ def test_conv2d_up2_phases(B, H, W, Cin, Cout, res, monkeypatch):
     r = torch.randn(B, 2 * H, 2 * W, Cout, device=DEV, generator=g).half() if res else None
     y = K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True, w_up2=wu)
     y9 = K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True)
-    monkeypatch.setenv("RDMI_UP2", "0")  # the default: phase weights given but not used
+    monkeypatch.setenv("RDMI_UP2", "0")  # phase weights given but not used
     assert torch.equal(K_.conv2d(x, wp, Cout, 3, upsample=True, bias=b, residual=r, gn=True, w_up2=wu), y9)
     monkeypatch.setenv("RDMI_UP2", "1")
     xin = F.interpolate(x.float().permute(0, 3, 1, 2), scale_factor=2.0, mode="nearest")
@@ -217,8 +221,14 @@ def test_conv2d_up2_phases(B, H, W, Cin, Cout, res, monkeypatch):
     if res:
         ref = ref + r.float().permute(0, 3, 1, 2)
     err, err9 = _rel(y.permute(0, 3, 1, 2), ref), _rel(y9.permute(0, 3, 1, 2), ref)
-    print(f"up2 B={B} {H}x{W} {Cin}->{Cout}: rel {err:.2e} (9-tap {err9:.2e})")
-    assert err < 4e-3
+    d = (y.float() - y9.float()).abs()
+    ulp = torch.exp2(torch.floor(torch.log2(y9.float().abs().clamp_min(2.0 ** -14))) - 10)
+    frac = (d > 0).float().mean().item()
+    print(f"up2 B={B} {H}x{W} {Cin}->{Cout}: rel {err:.2e} (9-tap {err9:.2e}); vs 9-tap: max {d.max().item():.2e}, "
+          f"{frac:.2e} of outputs differ, max {(d / ulp).max().item():.0f} ulp")
+    assert err < 4e-3 and abs(err - err9) < 1e-3
+    # ≤ 1 ulp of the value, or f32 summation noise (≪ the output's scale) where a result cancels to ~0
+    assert (d <= torch.clamp(ulp, min=1e-4 * ref.abs().max().item())).all() and frac < 0.05
     if (2 * H) % 32:
         assert torch.equal(y, y9)
     mr = K_.groupnorm_stats(y, 32, 1e-6)

@@ -3,7 +3,7 @@ every launch): per shape, time both settings alternately over several rounds and
 outputs are bitwise identical (the switches change the schedule, not the K order).
 
     python tools/conv_ab.py [--env RDMI_CONV_PIPE] [--rounds 3] [--iters 10]
-TF/s: the 9-tap algorithmic FLOPs (for RDMI_UP2 = 1 an effective rate: the phase form executes 4/9)."""
+TF/s: the 9-tap algorithmic FLOPs (for RDMI_UP2 = 1 an effective rate: the phase form executes 7/9)."""
 import argparse
 import math
 import os
@@ -34,6 +34,7 @@ CASES = [
     ("vae up 256 384->768 x8", 8, 384, 256, 256, True, "plain"),
     ("vae up 512 192->384 x8", 8, 192, 512, 512, True, "plain"),
     ("vae up 512 96->192 x8", 8, 96, 512, 512, True, "plain"),
+    ("unet up 640 48->96 x75", 75, 48, 640, 640, True, "plain"),
     ("unet 320 96^2 x48 full", 48, 96, 320, 320, False, "full"),
     ("unet 640 48^2 x48 full", 48, 48, 640, 640, False, "full"),
 ]
