@@ -48,6 +48,7 @@ struct AlP {
   double* fpart;  // [N][PS][4]: Σ|T|, Σ|Td|, min T, max T over pixel chunk c of frame f
   double *gs, *gt, *l1, *l2;  // [ntot][PS]: per snippet and pixel chunk
   float *m, *v;  // Adam moments [2*Ntot] (s then t)
+  const double* bct;  // [iters + 1][2]: Adam's bias corrections 1 − β1^step, 1 − β2^step (adam_bc_k)
   float* hist;
   int ntot;
 };
@@ -131,25 +132,54 @@ __device__ __forceinline__ void frame_stats_body(const AlP& p, int f, int c, flo
   double sa = 0.0, sd = 0.0;
   float mn = INFINITY, mx = -INFINITY;
   const long p1 = chunk_lo(p.P, c + 1);
-  for (long px = chunk_lo(p.P, c) + threadIdx.x; px < p1; px += 256) {
-    float sum = 0.f, sumd = 0.f;
-    for (int e = 0; e < cnt; ++e) {
-      float a = addrn(mulrn(ex[e][px], es[e]), et[e]);
-      float ac = fmaxf(a, 1e-3f);
-      sum = addrn(sum, a);
-      sumd = addrn(sumd, 1.0f / ac);
+  // UP pixels per thread per round, the covering slots' values loaded EB slots at a time: a round's
+  // loads are issued together instead of one dependent round trip per (pixel, slot).  The same sums
+  // in the same order (slots in row order per pixel, pixels in increasing order per thread).
+  constexpr int UP = 4, EB = 4;
+  for (long pb = chunk_lo(p.P, c) + threadIdx.x; pb < p1; pb += 256 * UP) {
+    float sum[UP], sumd[UP];
+#pragma unroll
+    for (int u = 0; u < UP; ++u) sum[u] = sumd[u] = 0.f;
+    for (int e0 = 0; e0 < cnt; e0 += EB) {
+      float xv[EB][UP];
+#pragma unroll
+      for (int q = 0; q < EB; ++q) {
+        const float* xr = ex[e0 + q < cnt ? e0 + q : cnt - 1];
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+          const long px = pb + 256L * u;
+          xv[q][u] = (e0 + q < cnt && px < p1) ? xr[px] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < EB; ++q) {
+        if (e0 + q >= cnt) break;
+        const float se = es[e0 + q], te = et[e0 + q];
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+          float a = addrn(mulrn(xv[q][u], se), te);
+          float ac = fmaxf(a, 1e-3f);
+          sum[u] = addrn(sum[u], a);
+          sumd[u] = addrn(sumd[u], 1.0f / ac);
+        }
+      }
     }
-    float T = 0.f, Td = 0.f;
-    if (cnt) {
-      T = sum / (float)cnt;
-      Td = sumd / (float)cnt;
+#pragma unroll
+    for (int u = 0; u < UP; ++u) {
+      const long px = pb + 256L * u;
+      if (px >= p1) break;
+      float T = 0.f, Td = 0.f;
+      if (cnt) {
+        T = sum[u] / (float)cnt;
+        Td = sumd[u] / (float)cnt;
+      }
+      p.T[(long)f * p.P + px] = T;
+      p.Td[(long)f * p.P + px] = Td;
+      sa += fabs((double)T);
+      sd += fabs((double)Td);
+      mn = fminf(mn, T);
+      mx = fmaxf(mx, T);
     }
-    p.T[(long)f * p.P + px] = T;
-    p.Td[(long)f * p.P + px] = Td;
-    sa += fabs((double)T);
-    sd += fabs((double)Td);
-    mn = fminf(mn, T);
-    mx = fmaxf(mx, T);
   }
   mn = wave_min(mn);
   mx = wave_max(mx);
@@ -207,26 +237,42 @@ __device__ __forceinline__ void snippet_grad_body(const AlP& p, int gk, int c, d
     const int f = k + j * p.stride[d];
     int kk = 0;
     if (row_owner(p, p.rb[d] + j, f, kk) != d) continue;  // overwritten by a later dilation's slot
-    float scf, scdf;
-    frame_scales(p, f, scf, scdf);
-    const float isc = 1.0f / scf, iscd = 1.0f / scdf;
     const float* Tf = p.T + (long)f * p.P;
     const float* Tdf = p.Td + (long)f * p.P;
-    for (long px = p0 + threadIdx.x; px < p1; px += 256) {
-      float xv = x[(long)j * p.P + px];
-      float a = addrn(mulrn(xv, s), t);
-      float z = a - Tf[px];
-      float ac = fmaxf(a, 1e-3f);
-      float ad = 1.0f / ac;
-      float zd = ad - Tdf[px];
-      float g1 = (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) * isc;
-      float g2 = 0.f;
-      if (a >= 1e-3f) g2 = (zd > 0.f ? 1.f : (zd < 0.f ? -1.f : 0.f)) * iscd * (-1.0f / (ac * ac));
-      double g = (double)g1 + (double)p.dw * (double)g2;
-      gs += g * (double)xv;
-      gt += g;
-      l1 += fabs((double)z) * (double)isc;
-      l2 += fabs((double)zd) * (double)iscd;
+    // UP pixels per thread per round: the round's operand loads and the frame's scale partials are
+    // issued together; the same terms accumulate in the same order (pixels increasing per thread)
+    constexpr int UP = 4;
+    for (long pb = p0 + threadIdx.x; pb < p1; pb += 256 * UP) {
+      float xa[UP], ta[UP], tda[UP];
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        const long px = pb + 256L * u;
+        const bool ok = px < p1;
+        xa[u] = ok ? x[(long)j * p.P + px] : 0.f;
+        ta[u] = ok ? Tf[px] : 0.f;
+        tda[u] = ok ? Tdf[px] : 0.f;
+      }
+      float scf, scdf;
+      frame_scales(p, f, scf, scdf);
+      const float isc = 1.0f / scf, iscd = 1.0f / scdf;
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        if (pb + 256L * u >= p1) break;
+        const float xv = xa[u];
+        float a = addrn(mulrn(xv, s), t);
+        float z = a - ta[u];
+        float ac = fmaxf(a, 1e-3f);
+        float ad = 1.0f / ac;
+        float zd = ad - tda[u];
+        float g1 = (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) * isc;
+        float g2 = 0.f;
+        if (a >= 1e-3f) g2 = (zd > 0.f ? 1.f : (zd < 0.f ? -1.f : 0.f)) * iscd * (-1.0f / (ac * ac));
+        double g = (double)g1 + (double)p.dw * (double)g2;
+        gs += g * (double)xv;
+        gt += g;
+        l1 += fabs((double)z) * (double)isc;
+        l2 += fabs((double)zd) * (double)iscd;
+      }
     }
   }
   double v[4] = {gs, gt, l1, l2};
@@ -308,8 +354,7 @@ __device__ __forceinline__ void hist_row(const AlP& p, int step, double denom, c
 // the soft-constraint term.  Returns the parameter value before the update.
 template <bool COHERENT>
 __device__ __forceinline__ float adam_param(const AlP& p, int i, int step, double denom) {
-  const double bc1 = 1.0 - pow((double)p.b1, (double)step);
-  const double bc2 = 1.0 - pow((double)p.b2, (double)step);
+  const double bc1 = p.bct[2 * step], bc2 = p.bct[2 * step + 1];
   const float step_size = (float)(p.lr / bc1);
   const float bc2s = (float)sqrt(bc2);
   const float lw = 1.0f - p.b1;   // lerp weight (1 - beta1)
@@ -415,6 +460,15 @@ __global__ __launch_bounds__(256) void aligner_history(AlP p, double denom, cons
     lo = mm[i * 2];
     hi = mm[i * 2 + 1];
   });
+}
+
+// Adam's bias corrections of every step, once per optimisation (the same double pow the update
+// evaluated per parameter before: two double pows off each iteration's critical path)
+__global__ void adam_bc_k(AlP p, int iters, double* bct) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i <= iters; i += gridDim.x * blockDim.x) {
+    bct[2 * i] = 1.0 - pow((double)p.b1, (double)i);
+    bct[2 * i + 1] = 1.0 - pow((double)p.b2, (double)i);
+  }
 }
 
 __global__ void zero_f32(float* x, long n) {
@@ -557,11 +611,12 @@ __global__ void prepare_k(PrepP p) {
 constexpr int HBLK = 128;
 
 // Workspace (floats): 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v
-// (2·ntot each), the per-snippet arrival counters (ntot, padded to 8 B); with a history, the
+// (2·ntot each), the per-snippet arrival counters (ntot, padded to 8 B), the bias-correction table
+// ((iters + 1)·2 doubles); with a history, the
 // fused loop's per-iteration slots for min(iters, HBLK) iterations: loss partials (2·ntot·PS
 // doubles), chunk min/max (2·N·PS) and pre-update parameters (2·ntot).
 long ws_floats(int N, long P, int ntot, int iters, bool hist) {
-  long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L);
+  long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L) + 4L * (iters + 1);
   const long slots = iters < HBLK ? iters : HBLK;
   if (hist) f += slots * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
   return f + 64;
@@ -625,9 +680,12 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   p.m = fw; fw += 2 * ntot;
   p.v = fw; fw += 2 * ntot;
   unsigned* cnt = (unsigned*)fw; fw += (ntot + 1) & ~1L;
+  double* bct = (double*)fw; fw += 4L * (a->iters + 1);
+  p.bct = bct;
   p.hist = a->history;
   const double denom = (double)p.R * p.N * (double)p.P;  // numel of the [Σw, N, P] loss tensor
   hipLaunchKernelGGL(zero_f32, dim3(16), dim3(256), 0, st, p.m, 4L * ntot + ((ntot + 1) & ~1L));  // m, v, cnt
+  hipLaunchKernelGGL(adam_bc_k, dim3(8), dim3(256), 0, st, p, a->iters, bct);
   int rc = rdmi::check_launch("aligner_zero");
   if (rc) return rc;
   if (fused_enabled()) {

@@ -247,7 +247,8 @@ def test_aligner_workspace_sizes_history_slots():
     """rdmi_aligner_workspace (host-only, no GPU): the fused aligner loop keeps per-iteration loss
     partials (2·ntot·PS doubles), chunk min/max (2·N·PS floats) and pre-update parameters (2·ntot)
     for one block of at most 128 iterations when a history is requested (aligner.hip HBLK: the
-    workspace does not grow with the iteration count), and nothing per iteration without one."""
+    workspace does not grow with the iteration count), and nothing per iteration without one — but
+    the Adam bias-correction table, 2 doubles per iteration (adam_bc_k)."""
     import ctypes as C
 
     from rollingdepth_amd import _native
@@ -260,13 +261,13 @@ def test_aligner_workspace_sizes_history_slots():
     a.iters = 2000
     a.history = None
     base = _native.lib.rdmi_aligner_workspace(C.byref(a))
-    assert base >= 8 * ntot * PS + 8 * 100 * PS + 2 * 100 * 5929 + 4 * ntot + ntot
+    assert base >= 8 * ntot * PS + 8 * 100 * PS + 2 * 100 * 5929 + 4 * ntot + ntot + 4 * 2001
     a.history = 1  # any non-null pointer: the size depends only on its presence
     with_hist = _native.lib.rdmi_aligner_workspace(C.byref(a))
     per_it = 4 * ntot * PS + 2 * 100 * PS + 2 * ntot
     assert 128 * per_it <= with_hist - base <= 128 * per_it + 64
     a.iters = 128
-    assert _native.lib.rdmi_aligner_workspace(C.byref(a)) == with_hist
+    assert _native.lib.rdmi_aligner_workspace(C.byref(a)) == with_hist - 4 * (2000 - 128)
     a.iters = 10
     assert _native.lib.rdmi_aligner_workspace(C.byref(a)) < with_hist
 
