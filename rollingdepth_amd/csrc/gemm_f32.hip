@@ -55,8 +55,8 @@ struct GemmF32P {
 
 constexpr unsigned OOB = 0x80000000u;
 
-__device__ __forceinline__ void dma16f(__amdgpu_buffer_rsrc_t r, unsigned voff, float* l) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, 0, 0, 0);
+__device__ __forceinline__ void dma16f(__amdgpu_buffer_rsrc_t r, unsigned voff, float* l, int soff = 0) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, soff, 0, 0);
 }
 
 // Epilogue: fragment (i, j) of a lane = output row mw + 16i + fr, channels nw + 16j + 4fq .. +3.
@@ -117,7 +117,7 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
       }
     }
   } else {
-    // GEGLU: within each wave's 64-column slab, columns [0,32) are the value half and [32,64) the
+    // GEGLU: within each 64-column slab of a wave, columns [0,32) are the value half and [32,64) the
     // gate half of output columns slab·32 + [0,32) (N % 128 == 0, weights row-interleaved).
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
@@ -125,21 +125,24 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
       if (m >= p.M) continue;
       const long crow = cb + (long)m * p.ldc;
 #pragma unroll
-      for (int j = 0; j < RN / 2; ++j) {
-        const int nh = nw + j * 16 + fq * 4;
-        const int no = nw / 2 + j * 16 + fq * 4;
-        const f32x4 bh = p.bias ? *(const f32x4*)(p.bias + nh) : f32x4{0.f, 0.f, 0.f, 0.f};
-        const f32x4 bg = p.bias ? *(const f32x4*)(p.bias + nh + 32) : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 o;
+      for (int sl = 0; sl < RN / 4; ++sl)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float h = acc[i][j][r] * p.alpha + bh[r];
-          const float g = acc[i][j + RN / 2][r] * p.alpha + bg[r];
-          o[r] = h * gelu_erf(g);
-          if (p.R) o[r] += p.R[rbz + (long)m * p.ldr + no + r];
+        for (int jj = 0; jj < 2; ++jj) {
+          const int j = 4 * sl + jj;
+          const int nh = nw + 64 * sl + jj * 16 + fq * 4;
+          const int no = nw / 2 + 32 * sl + jj * 16 + fq * 4;
+          const f32x4 bh = p.bias ? *(const f32x4*)(p.bias + nh) : f32x4{0.f, 0.f, 0.f, 0.f};
+          const f32x4 bg = p.bias ? *(const f32x4*)(p.bias + nh + 32) : f32x4{0.f, 0.f, 0.f, 0.f};
+          f32x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float h = acc[i][j][r] * p.alpha + bh[r];
+            const float g = acc[i][j + 2][r] * p.alpha + bg[r];
+            o[r] = h * gelu_erf(g);
+            if (p.R) o[r] += p.R[rbz + (long)m * p.ldr + no + r];
+          }
+          *(f32x4*)(p.C + crow + no) = o;
         }
-        *(f32x4*)(p.C + crow + no) = o;
-      }
     }
   }
 }
@@ -153,7 +156,10 @@ __device__ __forceinline__ void store_tile_f32(const GemmF32P& p, f32x4 (&acc)[R
 template <int MODE, int NP, int NS>
 __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P p) {
   constexpr bool X3 = NP == 2;
-  constexpr int BM = NP == 3 ? 64 : 128, BN = 128, NW = 4, WTM = BM / 2, WTN = 64;
+  // wave tiles: X3 32 × 128 (each wave splits only its own A rows: no A fragment is split twice in a
+  // workgroup), exact / X6 2 × 2 waves of BM/2 × 64
+  constexpr int WGN = NP == 2 ? 1 : 2;  // waves along N
+  constexpr int BM = NP == 3 ? 64 : 128, BN = 128, NW = 4, WTM = BM * WGN / NW, WTN = BN / WGN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
   constexpr int BH = NP == 3 ? 2 : 1;  // 128-B LDS rows per weight row and K-tile
   constexpr int AV = BM / 8 / NW, BV = BH * BN / 8 / NW;  // 1-KiB DMA instructions per wave per K-tile
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
   __shared__ __attribute__((aligned(16))) float lds[NS * SLOT];  // 96 / 64 / 80 KiB
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
   const int nbx = gridDim.x;
   const int logical = rdmi::xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
   int mt_, nt_;
@@ -205,48 +211,83 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
     const int n = n0 + q / BH;
     brow[i] = n < p.N ? n * (int)p.ldw + (q % BH) * BKF : -1;
   }
-  int tap = 0, cv = chunk;
-  if (MODE != 0) {
-    tap = chunk / p.cin_vecs;
-    cv = chunk - tap * p.cin_vecs;
-  }
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
+  const int wids = __builtin_amdgcn_readfirstlane(wid);
+  // Fast addressing (round 5): when a K-tile never straddles a tap (dense A, or Cin % 32 == 0) and
+  // lies inside Kvalid, a lane's A offset depends on the K-tile only through a wave-uniform step —
+  // the channel offset within the tap, or ks·BKF — which goes in the buffer instruction's scalar
+  // soffset; the per-lane row offsets (with the padding test) are recomputed only when the tap
+  // changes.  Out-of-range lanes keep an OOB voffset, still out of range after the soffset.
+  const bool fast = MODE == 0 || (p.cin_vecs % 8 == 0);
+  unsigned aoff[AV];
+  int atap = -1;
+  auto tap_offsets = [&](int t) {
+    const int dy = (t * 11) >> 5;  // t / 3 for t < 9
+    const int dx = t - 3 * dy;
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      if (MODE == 0) {
+        aoff[i] = ahb[i] == 0 ? (unsigned)(arow[i] + chunk * 4) * 4u : OOB;
+      } else {
+        const int hi = ahb[i] + dy, wi = awb[i] + dx;
+        const bool ok = (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
+        const int off = MODE == 1 ? arow[i] + (dy * p.IW + dx) * p.Cin + chunk * 4
+                                  : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + chunk * 4;
+        aoff[i] = ok ? (unsigned)off * 4u : OOB;
+      }
+    }
+  };
+  unsigned boff[BV];
+#pragma unroll
+  for (int i = 0; i < BV; ++i) boff[i] = brow[i] >= 0 ? (unsigned)(brow[i] + chunk * 4) * 4u : OOB;
 
   auto issue = [&](int ks, int slot) {
-    const int kk = ks * BKF + chunk * 4;
-    const bool kok = kk < p.Kvalid;
     float* la = lds + slot * SLOT;
     float* lb = la + BM * BKF;
-    if (MODE == 0) {
+    const bool whole = (ks + 1) * BKF <= p.Kvalid;  // wave-uniform
+    if (fast && whole) {
+      // K-tile ks: tap t0 = ks·BKF / Cin (uniform), channel step c0 within it
+      const int k0 = ks * BKF;
+      int t0 = 0, c0 = k0;
+      if (MODE != 0) {
+        t0 = k0 / p.Cin;
+        c0 = k0 - t0 * p.Cin;
+      }
+      if (t0 != atap) {  // wave-uniform
+        tap_offsets(t0);
+        atap = t0;
+      }
+#pragma unroll
+      for (int i = 0; i < AV; ++i) dma16f(ra_, aoff[i], la + (i * NW + wids) * 8 * BKF, c0 * 4);
+    } else if (MODE == 0) {
+      const int kk = ks * BKF + chunk * 4;
+      const bool kok = kk < p.Kvalid;
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
         const bool ok = ahb[i] == 0 && kok;
-        dma16f(ra_, ok ? (unsigned)(arow[i] + kk) * 4u : OOB, la + (i * NW + wid) * 8 * BKF);
+        dma16f(ra_, ok ? (unsigned)(arow[i] + kk) * 4u : OOB, la + (i * NW + wids) * 8 * BKF);
       }
     } else {
-      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9
-      const int dx = tap - 3 * dy;
-      const int tapoff = (dy * p.IW + dx) * p.Cin + cv * 4;
+      // general implicit im2col: this lane's (tap, channel chunk) of K-tile ks
+      const int kk = ks * BKF + chunk * 4;
+      const bool kok = kk < p.Kvalid;
+      int tl = kk / p.Cin;  // per lane
+      const int cl = (kk - tl * p.Cin) >> 2;
+      const int dy = (tl * 11) >> 5, dx = tl - 3 * dy;
+      const int tapoff = (dy * p.IW + dx) * p.Cin + cl * 4;
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
         const int hi = ahb[i] + dy, wi = awb[i] + dx;
         const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
-        const int off = MODE == 1 ? arow[i] + tapoff : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cv * 4;
-        dma16f(ra_, ok ? (unsigned)off * 4u : OOB, la + (i * NW + wid) * 8 * BKF);
-      }
-      cv += 8;
-      while (cv >= p.cin_vecs) {
-        cv -= p.cin_vecs;
-        ++tap;
+        const int off = MODE == 1 ? arow[i] + tapoff : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cl * 4;
+        dma16f(ra_, ok ? (unsigned)off * 4u : OOB, la + (i * NW + wids) * 8 * BKF);
       }
     }
-    const int kw = NP == 3 ? ks * 2 * BKF + chunk * 4 : kk;  // X6: a K-tile of W is 2 × 128 B per row
+    // W: X3 / X6 K-tiles are always whole (split parts, zero padded past K); exact f32 rows end at K
+    const int kst = NP == 3 ? ks * 2 * BKF : ks * BKF;  // X6: a K-tile of W is 2 × 128 B per row
+    const bool wok = NP > 1 || ks * BKF + chunk * 4 < p.Kvalid;
 #pragma unroll
-    for (int i = 0; i < BV; ++i) {
-      // X3 / X6: a K-tile of W is always whole (its split parts, zero padded past K)
-      const bool ok = brow[i] >= 0 && (NP > 1 || kok);
-      dma16f(rw_, ok ? (unsigned)(brow[i] + kw) * 4u : OOB, lb + (i * NW + wid) * 8 * BKF);
-    }
+    for (int i = 0; i < BV; ++i) dma16f(rw_, wok ? boff[i] : OOB, lb + (i * NW + wids) * 8 * BKF, kst * 4);
   };
 
   f32x4 acc[RM][RN];

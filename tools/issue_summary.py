@@ -14,7 +14,7 @@ import sys
 
 def last_launch(path):
     rows = list(csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))))
-    keep = [r for r in rows if any(k in r["Kernel_Name"] for k in ("attn_fwd", "conv_halo"))]
+    keep = [r for r in rows if any(k in r["Kernel_Name"] for k in ("attn_fwd", "conv_halo", "gemm_f32"))]
     did = max(int(r["Dispatch_Id"]) for r in keep)
     out = {r["Counter_Name"]: float(r["Counter_Value"]) for r in keep if int(r["Dispatch_Id"]) == did}
     r0 = next(r for r in keep if int(r["Dispatch_Id"]) == did)

@@ -58,6 +58,20 @@ elif a.what == "conv":
     act = B * H * W * C * 2
     print(f"algorithmic: read {2 * act + w.numel() * 2} B (input + residual + weights), write {act} B "
           f"(+ GroupNorm moments {C // 4 * B * H * W // 32 * 8} B); {2.0 * B * H * W * C * C * 9:.4e} FLOP")
+elif a.what == "f32conv":  # the f32 path's conv (RDMI_F32_X3 picks the product form at packing)
+    B, H, W, C = a.batch, a.res, a.res, a.cin
+    x = torch.randn(B, H, W, C, device="cuda")
+    w = K.pack_conv(torch.randn(C, C, 3, 3) / math.sqrt(C * 9), "cuda", C, torch.float32)
+    out = torch.empty(B, H, W, C, device="cuda")
+    fn = lambda: K.conv2d(x, w, C, 3, out=out)  # noqa: E731
+    print(f"f32 conv {B}x{H}x{W} {C}->{C}: {2.0 * B * H * W * C * C * 9:.4e} FLOP")
+elif a.what == "f32gemm":  # the f32 path's Linear (UNet L0 GEGLU-free projection shape by default)
+    M, N, Kd = a.batch * 9216, 3 * a.cin, a.cin
+    x = torch.randn(M, Kd, device="cuda")
+    w = K.pack_linear(torch.randn(N, Kd) / math.sqrt(Kd), "cuda", torch.float32)
+    out = torch.empty(M, N, device="cuda")
+    fn = lambda: K.gemm(x, w, Kd, out=out)  # noqa: E731
+    print(f"f32 gemm M={M} N={N} K={Kd}: {2.0 * M * N * Kd:.4e} FLOP")
 else:
     B, S, H = a.batch, 27648, 5
     C = H * 64
