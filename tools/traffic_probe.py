@@ -72,6 +72,14 @@ elif a.what == "f32gemm":  # the f32 path's Linear (UNet L0 GEGLU-free projectio
     out = torch.empty(M, N, device="cuda")
     fn = lambda: K.gemm(x, w, Kd, out=out)  # noqa: E731
     print(f"f32 gemm M={M} N={N} K={Kd}: {2.0 * M * N * Kd:.4e} FLOP")
+elif a.what == "f32attn":  # the f32 path's cross-frame attention (RDMI_F32_X3 / X6 pick the product form)
+    B, S, H = a.batch, 27648, 5
+    C = H * 64
+    qkv = torch.randn(B, S, 3 * C, device="cuda")
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    out = torch.empty(B, S, C, device="cuda")
+    fn = lambda: K.attention(q, k, v, H, out=out)  # noqa: E731
+    print(f"f32 attention: {4.0 * B * H * S * S * 64:.4e} FLOP")
 else:
     B, S, H = a.batch, 27648, 5
     C = H * 64
