@@ -460,7 +460,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     a.dtype = code
     a.Kp = kp
     aff = None
-    if in_gn is not None and not f32 and Cin % 64 == 0:
+    if in_gn is not None and not f32 and Cin % 64 == 0 and _gn_aff():
         # the norm's scale / shift table (rdmi.h in_affine): any Cin on the two-workgroups-per-CU halo
         # engine, each wave's 8 + 8 values loaded with the halo refill (for Cin <= 256 too: −2…4 %
         # against the LDS table built in the prologue, profiles/r05j_gn8_ab.log RDMI_CONV_GN8=0 columns
@@ -512,6 +512,13 @@ def _split_slots_aligned(B: int, elems_per_image: int, howo: int) -> bool:
         _split_slots_aligned(B - h, elems_per_image, howo)
 
 
+def _gn_aff() -> bool:
+    """RDMI_GN_AFF=0 (A/B): fused input GroupNorm without the scale / shift table (rdmi.h in_affine) —
+    the LDS table of the halo engines, so Cin ≤ 256 on the two-workgroups-per-CU engine and ≤ 1024 on
+    the 256-wide one (Cout % 256 == 0)."""
+    return os.environ.get("RDMI_GN_AFF", "1") != "0"
+
+
 def conv2d_in_gn_supported(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, groups: int, stride: int = 1,
                            pad: int = 1, upsample: bool = False, rowbias=None, out_hw=None) -> bool:
     """Whether rdmi_conv2d fuses an input GroupNorm for this conv (rdmi_conv2d_in_gn_supported)."""
@@ -520,7 +527,7 @@ def conv2d_in_gn_supported(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, 
     a = _conv_args(x, w, cout, k, stride, pad, None, upsample, None, None, rowbias, None, 1.0, Ho, Wo,
                    (None, None, None, groups, 0))
     a.dtype = _N.RDMI_F32 if x.dtype == F32 else _N.RDMI_F16
-    if x.dtype != F32 and Cin > 256 and Cin % 64 == 0:
+    if x.dtype != F32 and Cin > 256 and Cin % 64 == 0 and _gn_aff():
         a.in_affine = 16  # conv2d passes the scale / shift table here (the query reads no pointer)
     return bool(lib.rdmi_conv2d_in_gn_supported(C.byref(a)))
 
