@@ -8,7 +8,7 @@
 // geometry as the f16 engine's 64-half K-tiles — through a 3-slot LDS ring filled by
 // buffer-load-to-LDS DMA (no VGPR staging, two K-tiles in flight, one barrier per K-tile); ragged
 // M / N / K and the conv's implicit zero padding are out-of-range buffer offsets (zeros).  16-B
-// chunk c of LDS row r sits at c ^ (r & 7) (swizzled on the DMA source side).
+// chunk c of LDS row r sits at c ^ swz(r) (swizzled on the DMA source side; swz below).
 // Fragment reads: lane quarter q (lane >> 4) supplies k = 8q + s at MFMA step s (s = 0..7 per
 // K-tile) for BOTH operands, so a lane reads its 8 k values as two 16-B chunks (2q, 2q+1) per
 // fragment instead of eight 4-B reads; the sum over k is the same set of products.
@@ -54,6 +54,12 @@ struct GemmF32P {
 };
 
 constexpr unsigned OOB = 0x80000000u;
+
+// LDS image of a 128-B row r (32 floats / 64 bf16): 16-B chunk c at position c ^ swz(r & 15) (round 5).
+// The fragment reads of the 16x16 MFMA layouts — lane quarter q reads chunk 2q + h (f32 operands) or
+// q, 4 + q (bf16 parts) of rows fr = lane & 15 — are then conflict-free for ds_read_b128's lane groups
+// ({0-3, 12-15, 20-27}, ...); the former c ^ (r & 7) put the f32 reads 2-way on the same banks.
+__device__ __forceinline__ int swz(int r) { return ((r >> 1) & 1) ^ (((r >> 2) & 1) << 2) ^ (((r >> 3) & 1) * 6); }
 
 __device__ __forceinline__ void dma16f(__amdgpu_buffer_rsrc_t r, unsigned voff, float* l, int soff = 0) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)l, 16, voff, soff, 0, 0);
@@ -161,8 +167,9 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
   constexpr int WGN = NP == 2 ? 1 : 2;  // waves along N
   constexpr int BM = NP == 3 ? 64 : 128, BN = 128, NW = 4, WTM = BM * WGN / NW, WTN = BN / WGN;
   constexpr int RM = WTM / 16, RN = WTN / 16;
-  constexpr int BH = NP == 3 ? 2 : 1;  // 128-B LDS rows per weight row and K-tile
+  constexpr int BH = NP == 3 ? 2 : 1;  // 128 B of LDS per weight row and K-tile (X6: one 256-B row)
   constexpr int AV = BM / 8 / NW, BV = BH * BN / 8 / NW;  // 1-KiB DMA instructions per wave per K-tile
+  constexpr int WROW = BH * BKF;                           // floats per LDS weight row
   constexpr int LPS = AV + BV;
   constexpr int SLOT = (BM + BH * BN) * BKF;  // floats
   __shared__ __attribute__((aligned(16))) float lds[NS * SLOT];  // 96 / 64 / 80 KiB
@@ -181,11 +188,14 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.Wt + (long)bz * p.sW), (short)0, (int)p.w_bytes, 0x00020000);
 
   const int lrow = lane >> 3;
-  const int chunk = (lane & 7) ^ lrow;  // logical 4-float chunk this lane fetches
-  int arow[AV], ahb[AV], awb[AV];
+  // DMA instruction i of this wave fills 8 rows (i·NW + wid)·8 + lrow of 128 B; a lane fetches the
+  // logical 4-float chunk that lands at position lane & 7 of its row under the swizzle
+  int arow[AV], ahb[AV], awb[AV], achk[AV];
 #pragma unroll
   for (int i = 0; i < AV; ++i) {
-    const int m = m0 + (i * NW + wid) * 8 + lrow;
+    const int rt = (i * NW + wid) * 8 + lrow;
+    achk[i] = (lane & 7) ^ swz(rt & 15);
+    const int m = m0 + rt;
     const bool ok = m < p.M;
     const int mm = ok ? m : 0;
     if (MODE != 0) {
@@ -204,12 +214,15 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
       arow[i] = mm * (int)p.lda;
     }
   }
-  int brow[BV];  // LDS row q = (i·NW + wid)·8 + lrow holds weight row q / BH, 128-B half q % BH
+  // weights: 128-B rows as A; X6: 256-B rows (hi | mid | lo | zero per K-tile), instruction i filling
+  // rows (i·NW + wid)·4 + (lane >> 4), chunk c at position c ^ (row & 15)
+  int brow[BV], bchk[BV];
 #pragma unroll
   for (int i = 0; i < BV; ++i) {
-    const int q = (i * NW + wid) * 8 + lrow;
-    const int n = n0 + q / BH;
-    brow[i] = n < p.N ? n * (int)p.ldw + (q % BH) * BKF : -1;
+    const int q = NP == 3 ? (i * NW + wid) * 4 + (lane >> 4) : (i * NW + wid) * 8 + lrow;
+    bchk[i] = NP == 3 ? (lane & 15) ^ (q & 15) : (lane & 7) ^ swz(q & 15);
+    const int n = n0 + q;
+    brow[i] = n < p.N ? n * (int)p.ldw : -1;
   }
   const int Hl = p.IH << (MODE == 2 ? 1 : 0), Wl = p.IW << (MODE == 2 ? 1 : 0);
   const int wids = __builtin_amdgcn_readfirstlane(wid);
@@ -227,19 +240,19 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
       if (MODE == 0) {
-        aoff[i] = ahb[i] == 0 ? (unsigned)(arow[i] + chunk * 4) * 4u : OOB;
+        aoff[i] = ahb[i] == 0 ? (unsigned)(arow[i] + achk[i] * 4) * 4u : OOB;
       } else {
         const int hi = ahb[i] + dy, wi = awb[i] + dx;
         const bool ok = (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
-        const int off = MODE == 1 ? arow[i] + (dy * p.IW + dx) * p.Cin + chunk * 4
-                                  : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + chunk * 4;
+        const int off = MODE == 1 ? arow[i] + (dy * p.IW + dx) * p.Cin + achk[i] * 4
+                                  : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + achk[i] * 4;
         aoff[i] = ok ? (unsigned)off * 4u : OOB;
       }
     }
   };
   unsigned boff[BV];
 #pragma unroll
-  for (int i = 0; i < BV; ++i) boff[i] = brow[i] >= 0 ? (unsigned)(brow[i] + chunk * 4) * 4u : OOB;
+  for (int i = 0; i < BV; ++i) boff[i] = brow[i] >= 0 ? (unsigned)(brow[i] + bchk[i] * 4) * 4u : OOB;
 
   auto issue = [&](int ks, int slot) {
     float* la = lds + slot * SLOT;
@@ -260,34 +273,34 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
 #pragma unroll
       for (int i = 0; i < AV; ++i) dma16f(ra_, aoff[i], la + (i * NW + wids) * 8 * BKF, c0 * 4);
     } else if (MODE == 0) {
-      const int kk = ks * BKF + chunk * 4;
-      const bool kok = kk < p.Kvalid;
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
-        const bool ok = ahb[i] == 0 && kok;
+        const int kk = ks * BKF + achk[i] * 4;
+        const bool ok = ahb[i] == 0 && kk < p.Kvalid;
         dma16f(ra_, ok ? (unsigned)(arow[i] + kk) * 4u : OOB, la + (i * NW + wids) * 8 * BKF);
       }
     } else {
       // general implicit im2col: this lane's (tap, channel chunk) of K-tile ks
-      const int kk = ks * BKF + chunk * 4;
-      const bool kok = kk < p.Kvalid;
-      int tl = kk / p.Cin;  // per lane
-      const int cl = (kk - tl * p.Cin) >> 2;
-      const int dy = (tl * 11) >> 5, dx = tl - 3 * dy;
-      const int tapoff = (dy * p.IW + dx) * p.Cin + cl * 4;
 #pragma unroll
       for (int i = 0; i < AV; ++i) {
+        const int kk = ks * BKF + achk[i] * 4;
+        const bool kok = kk < p.Kvalid;
+        const int tl = kk / p.Cin;  // per lane
+        const int cl = kk - tl * p.Cin;
+        const int dy = (tl * 11) >> 5, dx = tl - 3 * dy;
         const int hi = ahb[i] + dy, wi = awb[i] + dx;
         const bool ok = kok && (unsigned)hi < (unsigned)Hl && (unsigned)wi < (unsigned)Wl;
-        const int off = MODE == 1 ? arow[i] + tapoff : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cl * 4;
+        const int off = MODE == 1 ? arow[i] + (dy * p.IW + dx) * p.Cin + cl
+                                  : arow[i] + ((hi >> 1) * p.IW + (wi >> 1)) * p.Cin + cl;
         dma16f(ra_, ok ? (unsigned)off * 4u : OOB, la + (i * NW + wids) * 8 * BKF);
       }
     }
     // W: X3 / X6 K-tiles are always whole (split parts, zero padded past K); exact f32 rows end at K
-    const int kst = NP == 3 ? ks * 2 * BKF : ks * BKF;  // X6: a K-tile of W is 2 × 128 B per row
-    const bool wok = NP > 1 || ks * BKF + chunk * 4 < p.Kvalid;
 #pragma unroll
-    for (int i = 0; i < BV; ++i) dma16f(rw_, wok ? boff[i] : OOB, lb + (i * NW + wids) * 8 * BKF, kst * 4);
+    for (int i = 0; i < BV; ++i) {
+      const bool wok = NP > 1 || ks * BKF + bchk[i] * 4 < p.Kvalid;
+      dma16f(rw_, wok ? boff[i] : OOB, lb + (i * NW + wids) * 8 * BKF, ks * WROW * 4);
+    }
   };
 
   f32x4 acc[RM][RN];
@@ -300,6 +313,7 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
   issue(0, 0);
   if (NS == 3) issue(1, 1);
   const int fr = lane & 15, fq = lane >> 4;
+  const int gfr = swz(fr);  // swizzle of every fragment row of this lane (rows ≡ fr mod 16)
   for (int kt = 0; kt < nk; ++kt) {
     if (NS == 3)
       rdmi::wait_vmcnt_only<LPS>();  // K-tile kt landed (kt+1 in flight)
@@ -310,16 +324,16 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
     asm volatile("" ::: "memory");
     issue(kt + NS - 1, (kt + NS - 1) % NS);  // into the slot read last in K-tile kt-1
     const float* la = lds + (kt % NS) * SLOT + (wm * WTM) * BKF;
-    const float* lb = lds + (kt % NS) * SLOT + BM * BKF + (wn * WTN) * BH * BKF;
+    const float* lb = lds + (kt % NS) * SLOT + BM * BKF + (wn * WTN) * WROW;
     if constexpr (NP == 3) {
       // lane quarter fq holds k = 8fq .. 8fq+7: A as f32 chunks 2fq, 2fq+1 split three ways; W as bf16
-      // chunks fq (hi) and 4+fq (mid) of LDS row 2·row, chunk fq (lo) of row 2·row + 1
+      // chunks fq (hi), 4+fq (mid) and 8+fq (lo) of its 256-B row
       bf16x8 as[RM][3], bs[RN][3];
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int row = i * 16 + fr;
-        const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ (row & 7)) << 2));
-        const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ (row & 7)) << 2));
+        const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ gfr) << 2));
+        const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ gfr) << 2));
         unsigned h[4], m[4], l[4];
         rdmi::split3_bf16x2(a0[0], a0[1], h[0], m[0], l[0]);
         rdmi::split3_bf16x2(a0[2], a0[3], h[1], m[1], l[1]);
@@ -331,10 +345,10 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
       }
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
-        const int q0 = 2 * (j * 16 + fr), q1 = q0 + 1;
-        bs[j][0] = *(const bf16x8*)(lb + q0 * BKF + ((fq ^ (q0 & 7)) << 2));
-        bs[j][1] = *(const bf16x8*)(lb + q0 * BKF + (((4 + fq) ^ (q0 & 7)) << 2));
-        bs[j][2] = *(const bf16x8*)(lb + q1 * BKF + ((fq ^ (q1 & 7)) << 2));
+        const float* wr = lb + (j * 16 + fr) * WROW;  // row ≡ fr mod 16
+        bs[j][0] = *(const bf16x8*)(wr + ((fq ^ fr) << 2));
+        bs[j][1] = *(const bf16x8*)(wr + (((4 + fq) ^ fr) << 2));
+        bs[j][2] = *(const bf16x8*)(wr + (((8 + fq) ^ fr) << 2));
       }
       // (weight part, activation part), largest first
       constexpr int wpart[6] = {0, 0, 1, 1, 0, 2}, apart[6] = {0, 1, 0, 1, 2, 0};
@@ -354,15 +368,15 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int row = i * 16 + fr;
-        const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ (row & 7)) << 2));
-        const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ (row & 7)) << 2));
+        const f32x4 a0 = *(const f32x4*)(la + row * BKF + (((2 * fq) ^ gfr) << 2));
+        const f32x4 a1 = *(const f32x4*)(la + row * BKF + (((2 * fq + 1) ^ gfr) << 2));
         rdmi::split_bf16x8(a0, a1, ah[i], al[i]);
       }
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int row = j * 16 + fr;
-        bh[j] = *(const bf16x8*)(lb + row * BKF + ((fq ^ (row & 7)) << 2));
-        bl[j] = *(const bf16x8*)(lb + row * BKF + (((4 + fq) ^ (row & 7)) << 2));
+        bh[j] = *(const bf16x8*)(lb + row * BKF + ((fq ^ gfr) << 2));
+        bl[j] = *(const bf16x8*)(lb + row * BKF + (((4 + fq) ^ gfr) << 2));
       }
 #pragma unroll
       for (int i = 0; i < RM; ++i)
@@ -381,12 +395,12 @@ __global__ __launch_bounds__(256, NS == 2 ? 2 : 1) void gemm_f32_kernel(GemmF32P
 #pragma unroll
       for (int i = 0; i < RM; ++i) {
         const int row = i * 16 + fr;
-        af[i] = *(const f32x4*)(la + row * BKF + ((lc ^ (row & 7)) << 2));
+        af[i] = *(const f32x4*)(la + row * BKF + ((lc ^ gfr) << 2));
       }
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int row = j * 16 + fr;
-        bf[j] = *(const f32x4*)(lb + row * BKF + ((lc ^ (row & 7)) << 2));
+        bf[j] = *(const f32x4*)(lb + row * BKF + ((lc ^ gfr) << 2));
       }
 #pragma unroll
       for (int s = 0; s < 4; ++s)
