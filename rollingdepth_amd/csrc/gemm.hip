@@ -174,6 +174,15 @@ bool h32_ok(const rdmi_conv_args* a, const GemmP& p, bool gn) {
          (!p.bias || ((uintptr_t)p.bias & 15) == 0) && (!gn || a->Cin <= 256);
 }
 
+// Streaming 1×1 conv (conv1x1.hip) for a dense 1×1 conv with a plain bias epilogue; RDMI_CONV1X1=0
+// keeps the GEMM engines (A/B; bitwise the same outputs)
+bool conv1x1_ok(const GemmP& p) {
+  const char* e = getenv("RDMI_CONV1X1");
+  if (e && e[0] == '0') return false;
+  return !p.R && !p.rowbias && !p.gnp && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 && p.ldw % 8 == 0 &&
+         (!p.bias || ((uintptr_t)p.bias & 15) == 0);
+}
+
 }  // namespace
 
 extern "C" int rdmi_conv2d_in_gn_supported(const rdmi_conv_args* a) {
@@ -293,6 +302,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     }
     return rdmi::check_launch("conv2d halo");
   }
+  if (dense && conv1x1_ok(p) && launch_conv1x1(p, a->Cin, a->Cout, (hipStream_t)stream))
+    return rdmi::check_launch("conv2d 1x1");
   return launch(p, 1, (hipStream_t)stream, false, dense ? 0 : (a->upsample ? 2 : 1));
 }
 

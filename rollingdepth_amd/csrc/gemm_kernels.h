@@ -2186,5 +2186,6 @@ void launch_gemm_occ2(int bn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_halo(int mode, int nph, int wn, bool gn, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_occ2(int mode, bool gn, bool pipe, dim3 g, hipStream_t s, const GemmP& p);
 void launch_conv_h32(bool gn, dim3 g, hipStream_t s, const GemmP& p);
+bool launch_conv1x1(const GemmP& p, int cin, int cout, hipStream_t st);  // false: no instance
 
 }  // namespace rdmi_gk

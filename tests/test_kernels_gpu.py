@@ -118,6 +118,28 @@ def test_conv2d(B, H, W, Cin, Cout, k, stride, pad, up, engine, h32):
     assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,bias", [(2, 24, 20, 256, 128, True), (1, 37, 29, 128, 256, True),
+                                                  (3, 16, 16, 128, 128, False), (2, 192, 192, 256, 128, True)])
+def test_conv1x1_stream_bitwise(B, H, W, Cin, Cout, bias, monkeypatch):
+    """The streaming 1×1 conv (conv1x1.hip, the VAE conv_shortcut shapes) against fp32, and bitwise
+    against the GEMM engines (RDMI_CONV1X1=0): the same MFMA per K-step, the same epilogue.  Ragged
+    last strip (1 073 pixels) and several strips per wave (73 728 pixels)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(B, Cin, H, W, device=DEV, generator=g).half()
+    w = (torch.randn(Cout, Cin, 1, 1, device=DEV, generator=g) / math.sqrt(Cin)).half()
+    b = torch.randn(Cout, device=DEV, generator=g) if bias else None
+    ref = F.conv2d(x.float(), w.float(), b)
+    xn = K_.nchw_to_nhwc(x, Cin)
+    wp = K_.pack_conv(w.float().cpu(), DEV, Cin)
+    monkeypatch.setenv("RDMI_CONV1X1", "1")
+    y = K_.conv2d(xn, wp, Cout, 1, pad=0, bias=b)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 4e-3
+    monkeypatch.setenv("RDMI_CONV1X1", "0")
+    y0 = K_.conv2d(xn, wp, Cout, 1, pad=0, bias=b)
+    assert torch.equal(y.view(torch.int16), y0.view(torch.int16))
+
+
 def test_conv2d_vae_downsample_rowbias_residual(engine):
     """Downsample2D with padding=0: F.pad(0,1,0,1) then 3x3 s2 (downsampling.py:141-146)."""
     K_ = _k()
