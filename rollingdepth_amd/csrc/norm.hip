@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void gn_from_partials(const float* __restrict_
 // registers) and walks rows; no per-element division, 16-B loads/stores.  SILU is a template
 // argument (dispatched once per launch): as a runtime flag hipcc if-converts it, computing and
 // discarding a SiLU per element of every non-SiLU apply.
-template <typename T, bool SILU>
+template <typename T, bool SILU, int U>
 __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x, T* __restrict__ y, long HW, int C,
                                                 int G, int rows_per_block, const float* __restrict__ mr,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta) {
@@ -216,9 +216,8 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x, T* __re
       sc[e] = rstd * gamma[c];
       sh[e] = beta[c] - mean * sc[e];
     }
-    for (long r = r0 + rl; r < r1; r += RL) {
-      float in[8], out[8];
-      ld8(xb + r * C + cv * 8, in);
+    auto apply = [&](const float (&in)[8], long r) __attribute__((always_inline)) {
+      float out[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float f = fmaf(in[e], sc[e], sh[e]);
@@ -226,6 +225,22 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x, T* __re
         out[e] = f;
       }
       st8(yb + r * C + cv * 8, out);
+    };
+    long r = r0 + rl;
+    // U rows per trip, their loads issued together (U × 16 B in flight per thread instead of one row):
+    // U = 4 moves 4.7-5.0 TB/s against 4.4-4.8 for one row (RDMI_GN_APPLY_U=1) and 4.5 for U = 8, bitwise
+    // the same outputs (tools/gn_apply_probe.py, profiles/r05zk_gn_apply_probe2.log)
+    for (; r + (U - 1) * RL < r1; r += U * RL) {
+      float in[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) ld8(xb + (r + u * RL) * C + cv * 8, in[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) apply(in[u], r + u * RL);
+    }
+    for (; r < r1; r += RL) {
+      float in[8];
+      ld8(xb + r * C + cv * 8, in);
+      apply(in, r);
     }
   }
 }
@@ -391,21 +406,29 @@ extern "C" int rdmi_groupnorm_apply(const void* x, void* y, int dtype, int B, lo
   rpb = (rpb + RL - 1) / RL * RL;
   dim3 g((unsigned)((HW + rpb - 1) / rpb), B);
   hipStream_t st = (hipStream_t)stream;
+  const char* ue = getenv("RDMI_GN_APPLY_U");
+  const bool u1 = ue && ue[0] == '1';
+#define RDMI_GN_APPLY(TT, S)                                                                                       \
+  do {                                                                                                             \
+    if (u1)                                                                                                        \
+      hipLaunchKernelGGL((gn_apply<TT, S, 1>), g, dim3(T), 0, st, (const TT*)x, (TT*)y, HW, C, G, (int)rpb, mean_rstd, \
+                         gamma, beta);                                                                             \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gn_apply<TT, S, 4>), g, dim3(T), 0, st, (const TT*)x, (TT*)y, HW, C, G, (int)rpb, mean_rstd, \
+                         gamma, beta);                                                                             \
+  } while (0)
   if (dtype == RDMI_F32) {
     if (silu)
-      hipLaunchKernelGGL((gn_apply<float, true>), g, dim3(T), 0, st, (const float*)x, (float*)y, HW, C, G, (int)rpb,
-                         mean_rstd, gamma, beta);
+      RDMI_GN_APPLY(float, true);
     else
-      hipLaunchKernelGGL((gn_apply<float, false>), g, dim3(T), 0, st, (const float*)x, (float*)y, HW, C, G, (int)rpb,
-                         mean_rstd, gamma, beta);
+      RDMI_GN_APPLY(float, false);
   } else {
     if (silu)
-      hipLaunchKernelGGL((gn_apply<f16, true>), g, dim3(T), 0, st, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
-                         mean_rstd, gamma, beta);
+      RDMI_GN_APPLY(f16, true);
     else
-      hipLaunchKernelGGL((gn_apply<f16, false>), g, dim3(T), 0, st, (const f16*)x, (f16*)y, HW, C, G, (int)rpb,
-                         mean_rstd, gamma, beta);
+      RDMI_GN_APPLY(f16, false);
   }
+#undef RDMI_GN_APPLY
   return rdmi::check_launch("groupnorm_apply");
 }
 
