@@ -24,7 +24,7 @@ FAMILIES = [
     ("attention_fwd_f32x6", re.compile(r"attn_fwd_f32s<3>|attn_fwd_f32sILi3E")),
     ("attention_fwd_f32x3", re.compile(r"attn_fwd_f32x3|attn_fwd_f32s<2>|attn_fwd_f32sILi2E")),
     ("attention_fwd_f32", re.compile(r"attn_fwd_f32")),
-    ("implicit_gemm", re.compile(r"conv_halo_kernel|conv_halo_occ2_kernel|gemm_pp_kernel|gemm_occ2_kernel|gemm_kernel<")),
+    ("implicit_gemm", re.compile(r"conv_halo_kernel|conv_halo_occ2_kernel|gemm_pp_kernel|gemm_occ2_kernel|gemm_kernel<|conv1x1_stream_kernel")),
     ("attention_fwd", re.compile(r"attn_fwd_d64")),
 ]
 
