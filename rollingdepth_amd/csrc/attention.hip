@@ -381,7 +381,11 @@ constexpr int TH = TK * 64;        // halves per K (or V) tile (8 KiB)
 constexpr int DPW = TK / 8 / NW;   // 8-row DMA pieces per wave per tile per tensor (2)
 }  // namespace pp
 
-template <int STAMP = 0>
+// NEGM (the dispatched form, round 5): −m̃ enters each QKᵀ chain as its initial accumulator, as in
+// attn_fwd_d64, instead of a fifth k-step (kone × qm below): 16 of 18 MFMAs per sub-tile → 16 of 16,
+// bitwise the same results, 3 % faster at L0 / L1 (profiles/r05zp_pipe_kb.log; 5 registers spill at two
+// workgroups per CU, and one workgroup per CU is 25 % slower).
+template <int STAMP = 0, bool NEGM = false>
 __global__ __launch_bounds__(64 * pp::NW, 2) void attn_fwd_d64_pipe(AttnP p) {
   constexpr int NW = pp::NW, QB = pp::QB, TK = pp::TK, NSL = pp::NSL, TH = pp::TH, DPW = pp::DPW;
   __shared__ __attribute__((aligned(16))) f16 lds[NSL * 2 * TH];  // 64 KiB: slot s = [K | V]
@@ -469,6 +473,7 @@ __global__ __launch_bounds__(64 * pp::NW, 2) void attn_fwd_d64_pipe(AttnP p) {
   // (and without the copies of them into each chain's accumulator)
   f16x8 kone = {}, qm[2] = {};
   if (hh == 0) kone[0] = (f16)1.0f;
+  f32x16 nm[2] = {};  // NEGM: −m̃ as the chain's initial accumulator (16 registers per block, no fifth MFMA)
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
@@ -515,10 +520,16 @@ __global__ __launch_bounds__(64 * pp::NW, 2) void attn_fwd_d64_pipe(AttnP p) {
   };
   // S'_qb = K·Qᵀ − m̃ (five chained MFMAs, the −m̃ step first)
   auto qk = [&](int qb) __attribute__((always_inline)) {
-    const f32x16 zero = {};
-    s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kone, qm[qb], zero, 0, 0, 0);
+    if constexpr (NEGM) {
+      s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[0], qf[qb][0], nm[qb], 0, 0, 0);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[ks], qf[qb][ks], s[qb], 0, 0, 0);
+      for (int ks = 1; ks < 4; ++ks) s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[ks], qf[qb][ks], s[qb], 0, 0, 0);
+    } else {
+      const f32x16 zero = {};
+      s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kone, qm[qb], zero, 0, 0, 0);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[ks], qf[qb][ks], s[qb], 0, 0, 0);
+    }
   };
   // Oᵀ_qb += Vᵀ·P_qbᵀ (two 16-key steps × two 32-row d-blocks)
   auto pv = [&](int qb) __attribute__((always_inline)) {
@@ -570,7 +581,12 @@ __global__ __launch_bounds__(64 * pp::NW, 2) void attn_fwd_d64_pipe(AttnP p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[qb][d][r] *= alpha;
       mt[qb] = mnew;
-      if (hh == 0) qm[qb][0] = (f16)(-mnew);
+      if constexpr (NEGM) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nm[qb][r] = -mnew;
+      } else if (hh == 0) {
+        qm[qb][0] = (f16)(-mnew);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[qb][r] -= delta;
       exps(qb, 0, 16);
@@ -1040,7 +1056,7 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
   static const bool f32sum = [] { const char* e = getenv("RDMI_ATTN_F32SUM"); return e && e[0] == '1'; }();
   const char* pe = getenv("RDMI_ATTN_PIPE");  // read per launch (A/B): 1 = the one-wave-per-SIMD pipeline
   if (pe && pe[0] == '1' && !f32sum) {
-    hipLaunchKernelGGL(attn_fwd_d64_pipe<0>, dim3(rdmi::div_up(Sq, pp::QB), H, B), dim3(64 * pp::NW), 0,
+    hipLaunchKernelGGL((attn_fwd_d64_pipe<0, true>), dim3(rdmi::div_up(Sq, pp::QB), H, B), dim3(64 * pp::NW), 0,
                        (hipStream_t)stream, p);
     return rdmi::check_launch("attention_fwd");
   }
