@@ -182,6 +182,47 @@ def test_groupnorm(C, G, HW, silu, eps):
     assert (y.float() - ref).abs().max().item() < 1e-2
 
 
+@pytest.mark.parametrize("C,HW,silu,dtype", [(512, 9216, True, torch.float16), (320, 1001, False, torch.float16),
+                                              (128, 37, True, torch.float16), (512, 2309, True, torch.float32),
+                                              (1280, 5, False, torch.float16)])
+def test_groupnorm_apply_row_unroll_bitwise(C, HW, silu, dtype, monkeypatch):
+    """gn_apply's four-rows-per-trip form (default) against one row per trip (RDMI_GN_APPLY_U=1): the same
+    per-element formula, so bitwise equal — ragged row counts exercise the tail loop."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(12)
+    x = (torch.randn(3, HW, C, device=DEV, generator=g) * 2 + 0.3).to(dtype)
+    gm = 1 + 0.1 * torch.randn(C, device=DEV, generator=g)
+    bt = 0.1 * torch.randn(C, device=DEV, generator=g)
+    monkeypatch.setenv("RDMI_GN_APPLY_U", "4")
+    y4 = K_.groupnorm(x, gm, bt, 32, 1e-6, silu)
+    monkeypatch.setenv("RDMI_GN_APPLY_U", "1")
+    y1 = K_.groupnorm(x, gm, bt, 32, 1e-6, silu)
+    iv = torch.int16 if dtype == torch.float16 else torch.int32
+    assert torch.equal(y4.view(iv), y1.view(iv))
+
+
+def test_conv1x1_stream_alpha_and_ld(monkeypatch):
+    """The streaming 1×1 conv with alpha ≠ 1 and a strided output (y_ld > Cout): bitwise the GEMM engines."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    B, H, W, Cin, Cout = 2, 33, 31, 256, 128
+    x = torch.randn(B, H, W, Cin, device=DEV, generator=g).half()
+    w = (torch.randn(Cout, Cin, 1, 1, device=DEV, generator=g) / math.sqrt(Cin)).half()
+    b = torch.randn(Cout, device=DEV, generator=g)
+    wp = K_.pack_conv(w.float().cpu(), DEV, Cin)
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RDMI_CONV1X1", mode)
+        big = torch.full((B, H, W, Cout + 64), float("nan"), dtype=torch.float16, device=DEV)
+        y = big[..., 16:16 + Cout]
+        K_.conv2d(x, wp, Cout, 1, pad=0, bias=b, alpha=0.18215, out=y)
+        outs.append(big)
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float()) * 0.18215 + b[None, :, None, None]
+    assert _rel(outs[0][..., 16:16 + Cout].permute(0, 3, 1, 2), ref) < 4e-3
+    assert torch.isnan(outs[0][..., :16]).all() and torch.isnan(outs[0][..., 16 + Cout:]).all()
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,up", [(2, 16, 16, 64, 128, False), (3, 12, 12, 128, 256, True),
                                                 (1, 24, 20, 256, 512, False), (2, 16, 32, 128, 256, False),
                                                 (2, 8, 8, 64, 256, True), (2, 16, 32, 128, 128, False),
