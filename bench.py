@@ -306,6 +306,29 @@ def _slice_main(a) -> int:
     return 0
 
 
+def _rank_times(marks, colls, steps: int, rank: int, wall_s: float) -> dict:
+    """This rank's per-phase and per-collective times over the timed steps (ms per step, HIP events on
+    the launch stream): phases between shard.sharded_forward's marks (encode, snippets, prepare,
+    aligner, merge, refine, egress); collectives summed by kind (all_gather / all_reduce / broadcast /
+    all_to_all) with their count and bytes per step, each span including any wait for the slowest rank."""
+    phases = {}
+    for tm in marks:
+        for (_, e0), (n1, e1) in zip(tm, tm[1:]):
+            phases[n1] = phases.get(n1, 0.0) + e0.elapsed_time(e1) / steps
+    coll = {}
+    for kind, e0, e1, nb in colls:
+        c = coll.setdefault(kind, {"ms": 0.0, "count": 0, "mbytes": 0.0})
+        c["ms"] += e0.elapsed_time(e1) / steps
+        c["count"] += 1
+        c["mbytes"] += nb / 1e6
+    for c in coll.values():
+        c["ms"] = round(c["ms"], 2)
+        c["count"] = c["count"] // steps
+        c["mbytes"] = round(c["mbytes"] / steps, 2)
+    return {"rank": rank, "wall_ms_per_step": round(wall_s / steps * 1e3, 1),
+            "phases_ms": {k: round(v, 1) for k, v in phases.items()}, "collectives": coll}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -387,10 +410,10 @@ def main():
     refine = pr["refine"]
     last = {}
 
-    def step():
+    def step(timing=None):
         if world > 1:
             so = sharded_forward(pipe, frames, list(dil0), pr["cap"], 3, coalign, init_noise=noise, num_frames=N,
-                                 to_host=True, refine_step=refine)
+                                 to_host=True, refine_step=refine, timing=timing)
             last["depth"] = so.depth_pred
             last["coaligned"] = so.depth_coaligned
             last["snip0"] = so.snippet_rows[0][0] if rank == 0 and so.snippet_rows[0].shape[0] else None
@@ -405,21 +428,30 @@ def main():
         step()
     torch.cuda.synchronize()
     K.profile_start()
+    marks = [[] for _ in range(a.steps)] if world > 1 else None
     if world > 1:
+        import rollingdepth_amd.shard as S
+        S.collective_timing = []
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for i in range(a.steps):
+        step(marks[i] if marks else None)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     prof = K.profile_stop()
+    per_rank = None
     if world > 1:
+        per_rank = _rank_times(marks, S.collective_timing, a.steps, rank, dt)
+        S.collective_timing = None
         tt = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = tt.item()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, per_rank)
+        per_rank = gathered
     validation = None
     if not a.no_validate:
         try:
@@ -479,6 +511,8 @@ def main():
                        "parallelism": f"snippet-dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "validation": validation,
         }
+        if per_rank is not None:
+            line["per_rank"] = per_rank
         if shared:
             line["rehearsal"] = "RDMI_BENCH_SHARED_GPU=1: all ranks on one GPU over gloo (not a scaling number)"
         print(json.dumps(line), flush=True)

@@ -330,26 +330,17 @@ int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, const float*
                        const float* const* t, const int* n, const int* stride, const int* w, int seq_len,
                        long HW, const float* shift, float* out, void* stream);
 
-/* Sharded merge: each rank sums s·x+t of ITS full-resolution snippets — rows
- * k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w_d][HW] — into sum_out [seq_len][HW] f64 (the
- * same per-slot arithmetic as rdmi_aligner_merge, zero where no local slot covers a frame); after a
- * reduce-scatter SUM by frame, rdmi_aligner_merge_finish divides frames f0 .. f0+nf-1 by their cover
- * count over all n[d] snippets.  With f32 arithmetic (x_f32 1 / 2) the f64 sums are order-independent
- * (exact while a frame's terms span ≤ ≈29 exponent bits, i.e. except in rare rounding cases), so any
- * world size and reduction order reproduces rdmi_aligner_merge bitwise in practice. */
-int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
-                               const float* const* t, const int* n, const int* stride, const int* k0,
-                               const int* nloc, const int* w, int seq_len, long HW, const float* shift, double* sum_out,
-                               void* stream);
-int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf, long HW,
-                              const double* sum, float* out, void* stream);
-/* Sharded merge over frame windows (round 5; replaces the full [seq_len, HW] reduce-scatter): each rank
- * sums only frames f0 .. f0+nf-1 — the window its own snippets cover — into sum_out [nf][HW] f64 (the
- * arithmetic of rdmi_aligner_merge_partial), sends every other rank the rows of that rank's frame chunk
- * (an all-to-all of uneven row counts), and rdmi_aligner_merge_finish_pieces adds the received pieces per
- * frame in source-rank order and divides by the frame's cover count: piece q = frames piece_f0[q] ..
- * piece_f0[q]+piece_nf[q]-1 of one source, pieces stored back to back in recv [Σ piece_nf][HW] f64, all
- * inside this rank's frames f0 .. f0+nf-1 (≤ 64 pieces) → out [nf][HW] f32. */
+/* Sharded merge over frame windows: each rank sums s·x+t of ITS full-resolution
+ * snippets — rows k0[d] .. k0[d]+nloc[d]-1 of dilation d, xf_d [nloc_d][w_d][HW] — over only frames
+ * f0 .. f0+nf-1 (the window its snippets cover) into sum_out [nf][HW] f64 (the per-slot arithmetic of
+ * rdmi_aligner_merge, zero where no local slot covers a frame), sends every other rank the rows of that
+ * rank's frame chunk (an all-to-all of uneven row counts), and rdmi_aligner_merge_finish_pieces adds the
+ * received pieces per frame in source-rank order and divides by the frame's cover count over all n[d]
+ * snippets: piece q = frames piece_f0[q] .. piece_f0[q]+piece_nf[q]-1 of one source, pieces stored back
+ * to back in recv [Σ piece_nf][HW] f64, all inside this rank's frames f0 .. f0+nf-1 → out [nf][HW] f32.
+ * Any piece count (the launch is split by frame range where more than 64 pieces arrive; a single frame
+ * touched by more than 64 pieces → RDMI_E_UNSUPPORTED).  With f32 arithmetic (x_f32 1 / 2) the f64 sums
+ * reproduce rdmi_aligner_merge bitwise in practice (exact while a frame's terms span ≤ ≈29 exponent bits). */
 int rdmi_aligner_merge_partial_window(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                       const float* const* t, const int* n, const int* stride, const int* k0,
                                       const int* nloc, const int* w, int f0, int nf, long HW, const float* shift,

@@ -102,11 +102,6 @@ _SIGS = {
     "rdmi_aligner_prepare": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rdmi_aligner_merge": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32),
                                  C.POINTER(i32), C.POINTER(i32), i32, i64, vp, vp, vp]),
-    "rdmi_aligner_merge_partial": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp), C.POINTER(i32),
-                                         C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i64,
-                                         vp, vp, vp]),
-    "rdmi_aligner_merge_finish": (i32, [i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), i32, i32, i64, vp, vp,
-                                        vp]),
     "rdmi_groupnorm_affine": (i32, [vp, vp, vp, i32, i32, i32, vp, vp]),
     "rdmi_aligner_merge_partial_window": (i32, [i32, C.POINTER(vp), i32, C.POINTER(vp), C.POINTER(vp),
                                                 C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),

@@ -504,7 +504,7 @@ __device__ __forceinline__ int cover_count(const int* n, const int* stride, int 
 
 // The f32-arithmetic merges (x_f32 1 / 2) add the slots' f32 terms s·x + t in f64: the sum of a
 // frame's few (≤ Σ w_d) f32 terms is exact whenever their exponents span ≤ ≈29 bits (all but rare
-// rounding cases), so it does not depend on the order the terms are added in — the sharded merge (per-rank partial sums, reduce-scatter in RCCL's order, finish)
+// rounding cases), so it does not depend on the order the terms are added in — the sharded merge (per-rank window sums, all-to-all, pieces added per frame, finish)
 // gives bitwise the single-GPU result, and both round once, at the mean.  The f16-emulating mode 0
 // (the reference's fp16 merge, RDMI_MERGE_F32=0) keeps its f32 running sum.
 __global__ void merge_k(MergeP p) {
@@ -544,17 +544,6 @@ __global__ void merge_k(MergeP p) {
       p.dsum[o] = p.xf32 ? dsum : (double)sum;
     else
       p.out[o] = p.xf32 ? (cnt ? (float)(dsum / (double)cnt) : 0.f) : (cnt ? sum / (float)cnt : 0.f);
-  }
-}
-
-// sharded merge, second half: out[f] = sum[f] / (number of covering slots of frame f0 + f over ALL
-// snippets), after the per-rank sums were reduced over ranks
-__global__ void merge_finish_k(MergeP p, const double* __restrict__ sum) {
-  const int fl = blockIdx.y;
-  const int cnt = cover_count(p.n, p.stride, p.nd, p.w, p.f0 + fl);
-  for (long px = blockIdx.x * (long)blockDim.x + threadIdx.x; px < p.HW; px += (long)gridDim.x * blockDim.x) {
-    const long i = (long)fl * p.HW + px;
-    p.out[i] = cnt ? (float)(sum[i] / (double)cnt) : 0.f;
   }
 }
 
@@ -774,14 +763,6 @@ extern "C" int rdmi_aligner_merge(int n_dil, const void* const* xf, int x_f32, c
                       stream);
 }
 
-extern "C" int rdmi_aligner_merge_partial(int n_dil, const void* const* xf, int x_f32, const float* const* s,
-                                          const float* const* t, const int* n, const int* stride, const int* k0,
-                                          const int* nloc, const int* w, int seq_len, long HW, const float* shift,
-                                          double* sum_out, void* stream) {
-  RDMI_REQUIRE(k0 && nloc && sum_out, RDMI_E_ARG, "aligner_merge_partial: k0/nloc/sum_out required");
-  return merge_launch(n_dil, xf, x_f32, s, t, n, stride, k0, nloc, w, 0, seq_len, HW, shift, nullptr, sum_out, stream);
-}
-
 extern "C" int rdmi_aligner_merge_partial_window(int n_dil, const void* const* xf, int x_f32, const float* const* s,
                                                  const float* const* t, const int* n, const int* stride, const int* k0,
                                                  const int* nloc, const int* w, int f0, int nf, long HW,
@@ -794,7 +775,7 @@ extern "C" int rdmi_aligner_merge_finish_pieces(int n_dil, const int* n, const i
                                                 int nf, long HW, int npieces, const int* piece_f0,
                                                 const int* piece_nf, const double* recv, float* out, void* stream) {
   RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && out && HW > 0 && f0 >= 0 && nf >= 0 &&
-                   npieces >= 0 && npieces <= MAXPIECES && (npieces == 0 || (piece_f0 && piece_nf && recv)),
+                   npieces >= 0 && (npieces == 0 || (piece_f0 && piece_nf && recv)),
                RDMI_E_ARG, "aligner_merge_finish_pieces: bad args");
   if (nf == 0) return 0;
   MergeP p{};
@@ -803,38 +784,48 @@ extern "C" int rdmi_aligner_merge_finish_pieces(int n_dil, const int* n, const i
     p.stride[d] = stride[d];
     p.w[d] = w[d];
   }
-  p.nd = n_dil; p.HW = HW; p.out = out; p.f0 = f0;
-  PiecesP q{};
+  p.nd = n_dil; p.HW = HW;
   long off = 0;
   for (int i = 0; i < npieces; ++i) {
     RDMI_REQUIRE(piece_nf[i] >= 0 && piece_f0[i] >= f0 && piece_f0[i] + piece_nf[i] <= f0 + nf, RDMI_E_ARG,
                  "aligner_merge_finish_pieces: piece %d frames %d+%d outside %d+%d", i, piece_f0[i], piece_nf[i], f0, nf);
-    q.pf0[i] = piece_f0[i];
-    q.pnf[i] = piece_nf[i];
-    q.poff[i] = off;
-    off += (long)piece_nf[i] * HW;
   }
-  q.np = npieces;
+  // The piece table travels in the kernel arguments (≤ MAXPIECES entries).  More pieces than that (one
+  // per source rank and dilation: 3·W > 64 from W = 22 ranks on) are split by frame: each launch takes
+  // a frame range and only the pieces that touch it, in their original (source-rank) order — every
+  // frame still adds all of its pieces in that order within one thread, so the sums are those of a
+  // single launch.  Only a single frame touched by more than MAXPIECES pieces is refused.
+  auto touches = [&](int i, int a, int b) { return piece_nf[i] > 0 && piece_f0[i] < b && piece_f0[i] + piece_nf[i] > a; };
   long gx = (HW + 255) / 256;
   if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(merge_finish_pieces_k, dim3((unsigned)gx, nf), dim3(256), 0, (hipStream_t)stream, p, q, recv);
-  return rdmi::check_launch("aligner_merge_finish_pieces");
-}
-
-extern "C" int rdmi_aligner_merge_finish(int n_dil, const int* n, const int* stride, const int* w, int f0, int nf,
-                                         long HW, const double* sum, float* out, void* stream) {
-  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && sum && out && HW > 0 && f0 >= 0 && nf >= 0,
-               RDMI_E_ARG, "aligner_merge_finish: bad args");
-  if (nf == 0) return 0;
-  MergeP p{};
-  for (int d = 0; d < n_dil; ++d) {
-    p.n[d] = n[d];
-    p.stride[d] = stride[d];
-    p.w[d] = w[d];
+  int fs = f0;
+  while (fs < f0 + nf) {
+    int fe = fs + 1, cnt = 0;
+    for (int i = 0; i < npieces; ++i) cnt += touches(i, fs, fe);
+    RDMI_REQUIRE(cnt <= MAXPIECES, RDMI_E_UNSUPPORTED,
+                 "aligner_merge_finish_pieces: frame %d is covered by %d pieces (at most %d)", fs, cnt, MAXPIECES);
+    while (fe < f0 + nf) {  // grow the range while its pieces still fit the table
+      int c2 = 0;
+      for (int i = 0; i < npieces; ++i) c2 += touches(i, fs, fe + 1);
+      if (c2 > MAXPIECES) break;
+      ++fe;
+    }
+    PiecesP q{};
+    off = 0;
+    for (int i = 0; i < npieces; ++i) {
+      if (touches(i, fs, fe)) {
+        q.pf0[q.np] = piece_f0[i];
+        q.pnf[q.np] = piece_nf[i];
+        q.poff[q.np] = off;
+        ++q.np;
+      }
+      off += (long)piece_nf[i] * HW;
+    }
+    p.f0 = fs;
+    p.out = out + (long)(fs - f0) * HW;
+    hipLaunchKernelGGL(merge_finish_pieces_k, dim3((unsigned)gx, fe - fs), dim3(256), 0, (hipStream_t)stream, p, q, recv);
+    if (int rc = rdmi::check_launch("aligner_merge_finish_pieces")) return rc;
+    fs = fe;
   }
-  p.nd = n_dil; p.HW = HW; p.out = out; p.f0 = f0;
-  long gx = (HW + 255) / 256;
-  if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(merge_finish_k, dim3((unsigned)gx, nf), dim3(256), 0, (hipStream_t)stream, p, sum);
-  return rdmi::check_launch("aligner_merge_finish");
+  return 0;
 }

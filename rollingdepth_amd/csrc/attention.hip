@@ -105,9 +105,9 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
   const int grp = wid >> 2;
   const int hh = lane >> 5;  // lane half
   const int c = lane & 31;
-  const int head = blockIdx.y;
-  const int b = blockIdx.z;
-  const int qi = blockIdx.x * QB + wid * 32 + c;
+  int qblk, head, b;
+  rdmi::xcd_block3(qblk, head, b);
+  const int qi = qblk * QB + wid * 32 + c;
 
   const f16* Q = p.q + (long)b * p.q_bs + head * 64;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
@@ -394,9 +394,9 @@ __global__ __launch_bounds__(64 * pp::NW, 2) void attn_fwd_d64_pipe(AttnP p) {
   const int wid = tid >> 6;
   const int hh = lane >> 5;
   const int c = lane & 31;
-  const int head = blockIdx.y;
-  const int b = blockIdx.z;
-  const int q0 = blockIdx.x * QB + wid * 64;  // query block qb of this wave: q0 + 32 qb + c
+  int qblk, head, b;
+  rdmi::xcd_block3(qblk, head, b);
+  const int q0 = qblk * QB + wid * 64;  // query block qb of this wave: q0 + 32 qb + c
 
   const f16* Q = p.q + (long)b * p.q_bs + head * 64;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(

@@ -53,10 +53,11 @@ __global__ __launch_bounds__(64 * NW5, 1) void attn_fwd_d512(Attn512P p) {
   const int wid = tid >> 6;
   const int hq = lane >> 4;   // lane quarter
   const int j16 = lane & 15;
-  const int b = blockIdx.y;
-  const int q = blockIdx.x * QB5 + wid * 16 + j16;
+  int qblk, b, z_;
+  rdmi::xcd_block3(qblk, b, z_);  // (query block, image): one XCD streams one image's K / Vᵀ
+  const int q = qblk * QB5 + wid * 16 + j16;
   // as the fix-up pass behind attn_fwd_d512_w4: only the 128-query blocks that pass flagged
-  if (p.flags && p.flags[b * gridDim.x + blockIdx.x] == 0) return;
+  if (p.flags && p.flags[b * gridDim.x + qblk] == 0) return;
 
   const f16* Q = p.q + (long)b * p.q_bs;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
@@ -235,8 +236,9 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_d512_w4(Attn512P p) {
   const int wid = tid >> 6;
   const int hh = lane >> 5;
   const int j32 = lane & 31;
-  const int b = blockIdx.y;
-  const int q = blockIdx.x * 128 + wid * 32 + j32;
+  int qblk, b, z_;
+  rdmi::xcd_block3(qblk, b, z_);
+  const int q = qblk * 128 + wid * 32 + j32;
 
   const f16* Q = p.q + (long)b * p.q_bs;
   const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_d512_w4(Attn512P p) {
   __syncthreads();
   if (lane == 0) badw[wid] = bad;
   __syncthreads();
-  if (tid == 0) p.flags[b * gridDim.x + blockIdx.x] = badw[0] | badw[1] | badw[2] | badw[3];
+  if (tid == 0) p.flags[b * gridDim.x + qblk] = badw[0] | badw[1] | badw[2] | badw[3];
   if (q < p.Sq && !bad) {
     const float inv = 1.f / l;
     f16* O = p.o + (long)b * p.o_bs + (long)q * p.o_ld;

@@ -43,8 +43,9 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32(AttnF32P p) {
   __shared__ __attribute__((aligned(16))) float vl[2][VTILE];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, qq = lane >> 4;
-  const int head = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * QBF + wid * QF * 16;
+  int qblk, head, b;
+  rdmi::xcd_block3(qblk, head, b);
+  const int q0 = qblk * QBF + wid * QF * 16;
   const float* Q = p.q + (long)b * p.q_bs + head * 64;
   const float* Kg = p.k + (long)b * p.k_bs + head * 64;
   const float* Vg = p.v + (long)b * p.v_bs + head * 64;
@@ -264,8 +265,9 @@ __global__ __launch_bounds__(64 * NWF, 1) void attn_fwd_f32s(AttnF32P p) {
   __shared__ __attribute__((aligned(16))) unsigned short vp[2][NP][64 * VT3];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fr = lane & 15, qq = lane >> 4;
-  const int head = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * QBF + wid * QF * 16;
+  int qblk, head, b;
+  rdmi::xcd_block3(qblk, head, b);
+  const int q0 = qblk * QBF + wid * QF * 16;
   const float* Q = p.q + (long)b * p.q_bs + head * 64;
   const float* Kg = p.k + (long)b * p.k_bs + head * 64;
   const float* Vg = p.v + (long)b * p.v_bs + head * 64;

@@ -48,6 +48,19 @@ __device__ __forceinline__ int xcd_remap(int bid, int total) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// The same remap for a 3-D grid (attention: x = query block, y = head, z = batch), x fastest: the
+// logical (x, y, z) of this workgroup.  Each XCD then runs consecutive query blocks of ONE (batch,
+// head), so the K / V they all sweep is streamed into that XCD's L2 once instead of into every XCD's
+// (in dispatch order the query blocks of a head are dealt round-robin to all 8 XCDs).
+__device__ __forceinline__ void xcd_block3(int& x, int& y, int& z) {
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int l = xcd_remap((blockIdx.z * ny + blockIdx.y) * nx + blockIdx.x, nx * ny * gridDim.z);
+  x = l % nx;
+  const int r = l / nx;
+  y = r % ny;
+  z = r / ny;
+}
+
 // logical tile → (m-tile, n-tile): groups of G m-tiles sweep all n-tiles with m fastest, so the
 // tiles an XCD runs together share G A-panels and a few B-panels (L2 reuse in both operands)
 __device__ __forceinline__ void tile_mn(int logical, int nbx, int nby, int G, int& mt, int& nt) {

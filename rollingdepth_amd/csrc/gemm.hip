@@ -154,7 +154,9 @@ bool halo_eligible(const rdmi_conv_args* a, int hmode) {
 
 // input GroupNorm: groups divide Cin; without in_affine the LDS scale/shift table holds ≤ 1024
 // channels (≤ 256 in the two-workgroups-per-CU variant, the only one for Cout % 256 != 0 other than
-// 128); with in_affine (the table in global memory, read per channel block) any Cin
+// 128); with in_affine (the table in global memory, read per channel block) any Cin — only
+// conv_halo_occ2_kernel reads that table, so rdmi_conv2d sends every in_affine conv to it whatever
+// RDMI_CONV_HALO selects (the 256-wide and 8-wave engines keep their fixed 1024-entry LDS table)
 bool in_gn_ok(const rdmi_conv_args* a) {
   const int cmax = a->in_affine ? (1 << 30) : (a->Cout % 256 == 0 || a->Cout == 128) ? 1024 : 256;
   return a->in_groups > 0 && a->Cin <= cmax && a->Cin % a->in_groups == 0;
@@ -282,7 +284,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
       p.Wt = (const f16*)a->w_up2; p.ldw = 7L * a->Cin; p.K = p.Kvalid = 7 * a->Cin;
       p.w_bytes = (unsigned)(4L * a->Cout * p.ldw * 2);
       launch_conv_occ2(3, false, p.conv_pipe != 0, dim3((a->Cout + 127) / 128, patches, 1), st, p);
-    } else if (a->Cout % 256 == 0 && !(hmode == 3 && (!gn || a->Cin <= 256 || p.gaff))) {
+    } else if (a->Cout % 256 == 0 && !p.gaff && !(hmode == 3 && (!gn || a->Cin <= 256))) {
       dim3 g(a->Cout / 256, patches, 1);
       const bool ph2 = hmode != 1 || gn;  // 2 phases per K-tile: +5-8 % over 4 (tools/kbench.py)
       if (a->upsample) {
@@ -290,10 +292,10 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
       } else {
         launch_conv_halo(1, ph2 ? 2 : 4, 4, ph2 && gn, g, st, p);
       }
-    } else if (a->Cout == 128 && (hmode == 4 || (gn && a->Cin > 256 && !p.gaff))) {  // the 8-wave 128-channel variant
+    } else if (a->Cout == 128 && !p.gaff && (hmode == 4 || (gn && a->Cin > 256))) {  // the 8-wave 128-channel variant
       dim3 g(1, patches, 1);
       launch_conv_halo(a->upsample ? 2 : 1, 1, 2, gn, g, st, p);
-    } else if (h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches
+    } else if (!p.gaff && h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches
       dim3 g(a->Cout / 128, (unsigned)((a->Ho / 8) * (a->Wo / 32) * a->B), 1);
       launch_conv_h32(gn, g, st, p);
     } else {  // two workgroups per CU (RDMI_CONV_HALO=3: also for Cout % 256 == 0)

@@ -46,6 +46,16 @@ def profile_stop():
 
 
 _PROF_SHAPES = os.environ.get("RDMI_PROF_SHAPES") == "1"  # key the timings by launch shape too
+# RDMI_PROF_SEQ=path (diagnostics, tools/traffic_split.py): every timed launch's (family, shape, FLOPs,
+# algorithmic bytes) in launch order, written to `path` at exit — matched 1:1 against the dispatches of a
+# rocprofv3 --pmc pass of the same process to split the fabric traffic per kernel and shape.
+_PROF_SEQ_PATH = os.environ.get("RDMI_PROF_SEQ")
+_PROF_SEQ = [] if _PROF_SEQ_PATH else None
+if _PROF_SEQ_PATH:
+    import atexit
+    import json as _json
+
+    atexit.register(lambda: _json.dump(_PROF_SEQ, open(_PROF_SEQ_PATH, "w")))
 
 
 class _Timed:
@@ -54,6 +64,8 @@ class _Timed:
 
     def __init__(self, name, flop, shape=None, nbytes=0):
         self.name, self.flop, self.nbytes, self.ev = name, flop, nbytes, None
+        if _PROF_SEQ is not None:
+            _PROF_SEQ.append((name, shape, flop, nbytes))
         if _PROF_SHAPES and shape is not None:
             self.name = f"{name} {shape}"
 
@@ -194,12 +206,31 @@ def pack_linear(w: torch.Tensor, device, dtype=F16) -> torch.Tensor:
     return _split_f32_weights(out, _f32_parts("linear")) if dtype == F32 else out
 
 
-def _w_code(a: torch.Tensor, w: torch.Tensor, name: str) -> int:
-    """dtype code of a GEMM/conv: the activations' dtype, or RDMI_F32_X3 for f32 activations
-    against split_bf16 weights."""
+def split_parts(w: torch.Tensor, kt: int, name: str = "weight") -> int:
+    """Part count of a bf16-split weight for reduction length kt: 2 (split_bf16, row 2·Kp) or 3
+    (split3_bf16, row 4·Kp), Kp = kt rounded up to 32; ValueError for any other row length or a
+    `_rdmi_parts` tag that contradicts it."""
+    kp = (kt + 31) // 32 * 32
+    row = w.shape[-1]
+    parts = {2 * kp: 2, 4 * kp: 3}.get(row)
+    tag = getattr(w, "_rdmi_parts", None)
+    if parts is None or (tag is not None and tag != parts):
+        raise ValueError(f"{name}: bf16-split weight row of {row} elements matches neither the x3 ({2 * kp}) "
+                         f"nor the x6 ({4 * kp}) layout of K = {kt}" +
+                         (f" (tagged _rdmi_parts={tag})" if tag is not None else ""))
+    return parts
+
+
+def _w_code(a: torch.Tensor, w: torch.Tensor, name: str, kt: int) -> int:
+    """dtype code of a GEMM/conv: the activations' dtype, or RDMI_F32_X3 / RDMI_F32_X6 for f32
+    activations against split_bf16 / split3_bf16 weights.  kt = the reduction length (K of a GEMM,
+    kh·kw·Cin of a conv).  The split layout is read from the weight's row length — 2·Kp (x3) or 4·Kp
+    (x6), Kp = kt rounded up to 32 — so a copy that dropped the `_rdmi_parts` tag still runs the right
+    engine, and a tag that disagrees with the row length fails loudly instead of running the other
+    engine on the wrong layout."""
     if a.dtype == F32 and w.dtype == BF16:
         _need(w, BF16, name)
-        return _N.RDMI_F32_X6 if getattr(w, "_rdmi_parts", 2) == 3 else _N.RDMI_F32_X3
+        return _N.RDMI_F32_X6 if split_parts(w, kt, name) == 3 else _N.RDMI_F32_X3
     _need(w, a.dtype, name)
     return _N.RDMI_F32 if a.dtype == F32 else _N.RDMI_F16
 
@@ -290,7 +321,7 @@ def gemm(a: torch.Tensor, w: torch.Tensor, k: int, out: Optional[torch.Tensor] =
     gn=True: the epilogue also emits the GroupNorm moments of the output (see _gn_part), which a
     following `groupnorm(out, ...)` consumes instead of re-reading the tensor."""
     _need_act(a, "gemm.a")
-    code = _w_code(a, w, "gemm.w")
+    code = _w_code(a, w, "gemm.w", k)
     f32 = a.dtype == F32
     out_f32 = out_f32 or f32
     batch = a.shape[0] if a.dim() == 3 else 1
@@ -414,7 +445,7 @@ def conv2d(x: torch.Tensor, w: torch.Tensor, cout: int, k: int, stride: int = 1,
     in_gn=(mean_rstd, gamma, beta, groups, silu): GroupNorm(+SiLU) of x applied as it is read
     (rdmi.h rdmi_conv_args.in_*; only where conv2d_in_gn_supported)."""
     _need_act(x, "conv2d.x")
-    code = _w_code(x, w, "conv2d.w")
+    code = _w_code(x, w, "conv2d.w", k * k * x.shape[-1])
     f32 = x.dtype == F32
     B, H, W, Cin = x.shape
     Ho, Wo = _out_hw(H, W, k, stride, pad, upsample, out_hw)
@@ -977,32 +1008,13 @@ def aligner_merge(xf: Sequence[torch.Tensor], scales, trans, strides, seq_len: i
     return out
 
 
-def aligner_merge_partial(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int], n: Sequence[int], scales, trans,
-                          strides, w: Sequence[int], seq_len: int, HW: int, shift: torch.Tensor, x_f32,
-                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Sharded merge, rank-local half: xf[d] [nloc_d, w_d, H, W] = global snippets k0[d] .. of dilation
-    d (None / 0 rows when the rank owns none) → f64 [seq_len, HW] per-frame sums of s·x+t (exact in
-    the f32-arithmetic modes, so the reduce-scatter order does not change the merged map)."""
-    nd = len(xf)
-    wv = (C.c_int * nd)(*list(w))
-    out = torch.empty((seq_len, HW), dtype=torch.float64, device=shift.device) if out is None else out
-    xp = (C.c_void_p * nd)(*[(x.data_ptr() if x is not None and x.shape[0] else None) for x in xf])
-    sp = (C.c_void_p * nd)(*[s.data_ptr() for s in scales])
-    tp = (C.c_void_p * nd)(*[t.data_ptr() for t in trans])
-    nn = (C.c_int * nd)(*list(n))
-    kk = (C.c_int * nd)(*list(k0))
-    nl = (C.c_int * nd)(*[(x.shape[0] if x is not None else 0) for x in xf])
-    stv = (C.c_int * nd)(*list(strides))
-    check(lib.rdmi_aligner_merge_partial(nd, xp, int(x_f32), sp, tp, nn, stv, kk, nl, wv, seq_len, HW,
-                                         shift.data_ptr(), out.data_ptr(), _stream()), "rdmi_aligner_merge_partial")
-    return out
-
-
 def aligner_merge_partial_window(xf: Sequence[Optional[torch.Tensor]], k0: Sequence[int], n: Sequence[int], scales,
                                  trans, strides, w: Sequence[int], f0: int, nf: int, HW: int, shift: torch.Tensor,
                                  x_f32, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """aligner_merge_partial restricted to frames f0 .. f0+nf-1 (a range the rank's snippets cover)
-    → f64 [nf, HW] (`out`: a contiguous f64 [nf, HW] view to write into)."""
+    """Sharded merge, rank-local half (rdmi_aligner_merge_partial_window): xf[d] [nloc_d, w_d, H, W] =
+    global snippets k0[d] .. of dilation d (None / 0 rows when the rank owns none) → f64 [nf, HW] sums of
+    s·x+t over frames f0 .. f0+nf-1 (a range the rank's snippets cover; `out`: a contiguous f64 [nf, HW]
+    view to write into)."""
     nd = len(xf)
     if out is None:
         out = torch.empty((nf, HW), dtype=torch.float64, device=shift.device)
@@ -1038,23 +1050,6 @@ def aligner_merge_finish_pieces(recv: torch.Tensor, pieces: Sequence[Tuple[int, 
     check(lib.rdmi_aligner_merge_finish_pieces(nd, nn, stv, wv, f0, nf, HW, npc, pf, pn,
                                                recv.data_ptr() if recv.numel() else None, out.data_ptr(),
                                                _stream()), "rdmi_aligner_merge_finish_pieces")
-    return out
-
-
-def aligner_merge_finish(sums: torch.Tensor, n: Sequence[int], strides: Sequence[int], w: Sequence[int],
-                         f0: int) -> torch.Tensor:
-    """Sharded merge, after the reduce-scatter: f64 [nf, HW] sums of frames f0 .. → f32 per-frame means
-    (w: snippet length per dilation)."""
-    if sums.dtype != torch.float64:
-        raise TypeError("aligner_merge_finish: f64 sums expected (aligner_merge_partial)")
-    nf, HW = sums.shape
-    nd = len(n)
-    out = torch.empty((nf, HW), dtype=F32, device=sums.device)
-    nn = (C.c_int * nd)(*list(n))
-    stv = (C.c_int * nd)(*list(strides))
-    wv = (C.c_int * nd)(*list(w))
-    check(lib.rdmi_aligner_merge_finish(nd, nn, stv, wv, f0, nf, HW, sums.data_ptr(), out.data_ptr(), _stream()),
-          "rdmi_aligner_merge_finish")
     return out
 
 

@@ -13,8 +13,11 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Per f
        per-snippet depth before co-alignment);
        every rank runs the same deterministic 2000-iteration Adam kernel on the same inputs, so every
        rank holds the same scales / translations with no broadcast;
-       merge_scaled_triplets (:231-262) as rank-local per-frame sums of s·x+t over the rank's own
-       full-resolution snippets, reduce-scatter SUM by frame chunk, ÷ the frame's cover count;
+       merge_scaled_triplets (:231-262) windowed: each rank sums s·x+t (f64) over only the frame
+       ranges its own full-resolution snippets cover, one uneven all-to-all sends those rows to the
+       owners of the frame chunks, and each owner adds the received pieces per frame in source-rank
+       order and divides by the frame's cover count (no world-size limit: the library splits a piece
+       table wider than its 64-entry kernel argument by frame range);
        all-reduce MIN / MAX for the renormalisation (rollingdepth_pipeline.py:316-318);
   4. refine (full / paper presets): each rank encodes its chunk of the co-aligned depth, the depth
      latents are all-gathered, and every refine step splits its snippets over the ranks with one
@@ -93,27 +96,60 @@ def _via_host(group, t: torch.Tensor) -> bool:
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
+# Per-collective timing (bench.py --gpus N): when a list, every collective below appends (kind, start
+# event, end event, bytes) — HIP events recorded on the current stream right before the collective is
+# issued and right after the current stream was made to wait for it, so a span covers the transfer plus
+# any wait for the slowest rank to arrive.
+collective_timing: Optional[list] = None
+
+
+class _Coll:
+    """Brackets one collective with timing events when `collective_timing` is a list."""
+
+    def __init__(self, kind: str, nbytes: int):
+        self.kind, self.nbytes = kind, nbytes
+
+    def __enter__(self):
+        if collective_timing is not None:
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+        return self
+
+    def __exit__(self, *exc):
+        if collective_timing is not None and exc[0] is None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            collective_timing.append((self.kind, self.e0, e1, self.nbytes))
+        return False
+
+
+def _nbytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
+
+
 def _gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
     if isinstance(group, SliceGroup):  # every rank's slot gets this rank's rows
         out.view(-1, inp.numel()).copy_(inp.reshape(1, -1).expand(out.numel() // max(inp.numel(), 1), -1))
         return
-    if _via_host(group, inp):
-        o = out.cpu()
-        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
-        out.copy_(o)
-    else:
-        dist.all_gather_into_tensor(out, inp, group=group)
+    with _Coll("all_gather", _nbytes(out)):
+        if _via_host(group, inp):
+            o = out.cpu()
+            dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=group)
 
 
 def _all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None):
     if isinstance(group, SliceGroup):
         return
-    if _via_host(group, t):
-        h = t.cpu()
-        dist.all_reduce(h, op=op, group=group)
-        t.copy_(h)
-    else:
-        dist.all_reduce(t, op=op, group=group)
+    with _Coll("all_reduce", _nbytes(t)):
+        if _via_host(group, t):
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=group)
 
 
 def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) -> torch.Tensor:
@@ -127,38 +163,18 @@ def _all_gather_rows(local: torch.Tensor, total: int, world: int, group=None) ->
     return out[:total]
 
 
-def _reduce_scatter_rows(full: torch.Tensor, world: int, group=None) -> torch.Tensor:
-    """SUM over ranks of `full` [total, ...], rank r keeping rows chunk_bounds(total, world)[r]."""
-    total = full.shape[0]
-    c = (total + world - 1) // world
-    if c * world != total:
-        full = torch.cat([full, torch.zeros((c * world - total, *full.shape[1:]), dtype=full.dtype,
-                                            device=full.device)])
-    out = torch.empty((c, *full.shape[1:]), dtype=full.dtype, device=full.device)
-    if isinstance(group, SliceGroup):
-        out.copy_(full[group.rank * c:(group.rank + 1) * c])
-    elif _via_host(group, full):
-        o = out.cpu()
-        dist.reduce_scatter_tensor(o, full.contiguous().cpu(), group=group)
-        out.copy_(o)
-    else:
-        dist.reduce_scatter_tensor(out, full.contiguous(), group=group)
-    rank = _rank(group)
-    lo, hi = chunk_bounds(total, world)[rank]
-    return out[:hi - lo]
-
-
 def _broadcast(t: torch.Tensor, src: int = 0, group=None):
     """Broadcast from the group's rank `src` (device tensors staged through the host under gloo)."""
     if isinstance(group, SliceGroup):
         return
     root = dist.get_global_rank(group, src) if group is not None and group != dist.group.WORLD else src
-    if _via_host(group, t):
-        h = t.cpu()
-        dist.broadcast(h, root, group=group)
-        t.copy_(h)
-    else:
-        dist.broadcast(t, root, group=group)
+    with _Coll("broadcast", _nbytes(t)):
+        if _via_host(group, t):
+            h = t.cpu()
+            dist.broadcast(h, root, group=group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, root, group=group)
 
 
 def gather_rows_by_dilation(local: Sequence[torch.Tensor], counts: Sequence[int], world: int,
@@ -238,7 +254,7 @@ def _merge_windowed(rows, k0, counts, scales, trans, strides, slens, N: int, HW:
     """merge_scaled_triplets over W ranks: per-rank f64 sums of only the frames its snippets cover, an
     all-to-all of the rows each rank's frame chunk needs (uneven row counts; RCCL over xGMI), then
     the received pieces added per frame in source-rank order and ÷ the cover count (f64 sums: the
-    single-GPU merge bitwise, as the full reduce-scatter it replaces).  Returns this rank's chunk
+    single-GPU merge bitwise).  Returns this rank's chunk
     [f1 − f0, HW] f32.  Moves each rank's covered frames instead of N·HW·8 B per rank."""
     from . import kernels as K
 
@@ -272,12 +288,14 @@ def exchange_window_rows(sums: torch.Tensor, send: Sequence[int], recv: Sequence
                 rbuf.view(-1).copy_(src.repeat(reps)[:rbuf.numel()])
             else:
                 rbuf.zero_()
-    elif _via_host(group, sums):
-        h = torch.empty(rbuf.shape, dtype=rbuf.dtype)
-        dist.all_to_all_single(h.view(-1), sums.reshape(-1).cpu(), out_split, in_split, group=group)
-        rbuf.copy_(h)
     else:
-        dist.all_to_all_single(rbuf.view(-1), sums.reshape(-1), out_split, in_split, group=group)
+        with _Coll("all_to_all", max(_nbytes(sums), _nbytes(rbuf))):
+            if _via_host(group, sums):
+                h = torch.empty(rbuf.shape, dtype=rbuf.dtype)
+                dist.all_to_all_single(h.view(-1), sums.reshape(-1).cpu(), out_split, in_split, group=group)
+                rbuf.copy_(h)
+            else:
+                dist.all_to_all_single(rbuf.view(-1), sums.reshape(-1), out_split, in_split, group=group)
     return rbuf
 
 

@@ -101,7 +101,7 @@ def test_aligner_merge_f16_rounding():
     assert np.abs(got - ref[:, 0].astype(np.float32)).max() <= 2e-3
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("world", [2, 3, 8, 24])
 @pytest.mark.parametrize("f32", [False, True])
 def test_aligner_merge_windowed_bitwise(world, f32):
     """The sharded merge over frame windows (round 5: rdmi_aligner_merge_partial_window per rank, the
@@ -147,6 +147,32 @@ def test_aligner_merge_windowed_bitwise(world, f32):
         pieces = [pc for src in recv for pc in src]
         got.append(K.aligner_merge_finish_pieces(rbuf.contiguous(), pieces, n, dil, w, f0, f1 - f0, HW))
     assert torch.equal(torch.cat(got), ref)
+
+
+def test_aligner_merge_finish_many_pieces():
+    """More pieces than the kernel's 64-entry argument table (3 dilations × W ≥ 22 source ranks): the
+    library splits the launch by frame range, each launch taking the pieces that touch its frames in
+    their original order — bitwise the per-frame launches of ≤ 64 pieces each."""
+    from rollingdepth_amd import kernels as K
+
+    N, HW = 30, 200
+    n, dil, w = [N - 2, N - 2 * 5, N - 2 * 9], [1, 5, 9], [3, 3, 3]
+    rng = np.random.default_rng(7)
+    pieces = []
+    for _ in range(150):  # source-rank order: arbitrary overlapping windows
+        a = int(rng.integers(0, N))
+        pieces.append((a, int(rng.integers(0, min(4, N - a) + 1))))
+    rows = sum(p[1] for p in pieces)
+    recv = torch.from_numpy(rng.standard_normal((rows, HW))).to(DEV)
+    got = K.aligner_merge_finish_pieces(recv, pieces, n, dil, w, 0, N, HW)
+    offs = np.cumsum([0] + [p[1] for p in pieces])
+    for f in range(N):
+        sel = [i for i, p in enumerate(pieces) if p[1] and p[0] <= f < p[0] + p[1]]
+        assert len(sel) <= 64
+        # each touching piece clipped to frame f (one row), in the same order
+        sub = torch.cat([recv[offs[i] + f - pieces[i][0]][None] for i in sel]) if sel else recv[:0]
+        ref = K.aligner_merge_finish_pieces(sub.contiguous(), [(f, 1)] * len(sel), n, dil, w, f, 1, HW)
+        assert torch.equal(got[f:f + 1], ref), f
 
 
 @pytest.mark.parametrize("case", ["small", "mixed", "metric"])

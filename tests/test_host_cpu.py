@@ -89,6 +89,26 @@ def test_split_bf16_layout(monkeypatch):
     assert c.dtype == torch.bfloat16 and c.shape == (4, 2 * 384)
 
 
+def test_split_weight_engine_from_row_length():
+    """The x3 / x6 engine is chosen from the bf16 weight's row length (2·Kp / 4·Kp), so a copy that
+    lost the `_rdmi_parts` tag still runs the right engine; a row length matching neither layout, or a
+    tag contradicting it, raises instead of running an engine on the wrong layout."""
+    from rollingdepth_amd import kernels as K
+
+    w = torch.randn(6, 70)
+    x3 = K.split_bf16(torch.nn.functional.pad(w, (0, 26)))
+    x6 = K.split3_bf16(torch.nn.functional.pad(w, (0, 26)))
+    assert K.split_parts(x3, 70) == 2
+    assert K.split_parts(x6, 70) == 3
+    assert K.split_parts(x6.clone(), 70) == 3  # the clone dropped the tag
+    with pytest.raises(ValueError):
+        K.split_parts(x3[:, :160], 70)
+    bad = x3.clone()
+    bad._rdmi_parts = 3
+    with pytest.raises(ValueError):
+        K.split_parts(bad, 70)
+
+
 def test_pack_conv_up2_phase_identity():
     """pack_conv_up2: conv3×3(nearest×2(x)) == the four 2×2 phase convs on the source grid with
     merged weights hi + lo (rdmi.h rdmi_conv_args.w_up2) — the identity the GPU's phase-decomposed

@@ -326,7 +326,10 @@ def test_groupnorm_moments_from_gemm(engine):
     (2, 16, 64, 128, 128, False, True, 32), (1, 16, 32, 256, 128, False, True, 32), (2, 16, 32, 128, 128, False, False, 32),
     # Cin > 256 through the scale / shift table (rdmi.h in_affine) on the two-workgroups-per-CU engine
     (2, 16, 16, 640, 320, False, True, 32), (1, 32, 16, 960, 320, False, True, 32), (2, 16, 16, 512, 128, False, True, 32),
-    (1, 16, 16, 1280, 640, False, True, 32), (1, 8, 8, 512, 512, True, True, 32)])
+    (1, 16, 16, 1280, 640, False, True, 32), (1, 8, 8, 512, 512, True, True, 32),
+    # Cin > 1024 with Cout % 256 == 0 / Cout == 128: under halo256 / halo128w8 these must still reach the
+    # engine that reads the in_affine table (the others hold a 1024-entry LDS table)
+    (1, 32, 32, 1280, 1280, False, True, 32), (1, 16, 16, 1280, 128, False, True, 32)])
 def test_conv2d_fused_input_groupnorm(B, H, W, Cin, Cout, up, silu, G, engine, h32):
     """GroupNorm(+SiLU) applied inside the halo conv's input path (rdmi_conv_args.in_*) against the
     unfused groupnorm → conv2d pair on the same data: the same normalised f16 values feed the same

@@ -311,7 +311,7 @@ def _rccl_world1():
                                            ("tiny_pipeline", (36, 27))])
 def test_sharded_forward_world1_equals_forward(name, frame_hw):
     """shard.sharded_forward over a 1-rank RCCL group (aligner-input all-gather, every-rank aligner,
-    merge partial sums + reduce-scatter + cover-count finish, sharded refine all-reduce) reproduces
+    windowed merge sums + all-to-all + cover-count finish, sharded refine all-reduce) reproduces
     pipe.forward bitwise — including a frame size whose latent is not H/8 (36×27 → 18×13 padded
     stride-2 levels; decoded 8h × 8w)."""
     from rollingdepth_amd.pipeline import RollingDepthPipeline

@@ -1,11 +1,12 @@
 """World-size-2 (and 3) gloo tests (CPU) of the multi-GPU plan of rollingdepth_amd/shard.py
 (SURVEY.md §8e).  The collectives and the rank/frame/snippet bookkeeping are the product's own
-functions; the per-rank device kernels (rdmi_aligner_merge_partial / rdmi_snippet_accumulate) are
+functions; the per-rank device kernels (rdmi_aligner_merge_partial_window / rdmi_snippet_accumulate) are
 stood in for by a CPU restatement of their contract (the GPU tests check the kernels against the
 single-GPU merge and refine).  Checked against the oracle's single-process merge / refine average:
   * the flat snippet split + all-gather of per-snippet aligner inputs reassembles every dilation;
   * all-reduce MIN of [min, −max] gives the global min / max;
-  * per-rank merge sums + reduce-scatter by frame + ÷ cover count == merge_scaled_triplets;
+  * windowed merge: per-rank sums over the frames its snippets cover + all-to-all of each frame chunk's
+    rows + ÷ cover count == merge_scaled_triplets;
   * per-rank refine sums + all-reduce + ÷ cover count == the single-process snippet average.
 """
 import os
@@ -30,9 +31,9 @@ def _snippet(d, k, shape):
 
 
 def _merge_partial_cpu(rows, k0, n, strides, scales, trans, w, N, HW):
-    """CPU restatement of rdmi_aligner_merge_partial (f32 snippets): per frame the sum over this
-    rank's (dilation, local snippet, slot) of s·x + t, slots in the reference's k-ascending order
-    (w: snippet length per dilation)."""
+    """CPU restatement of rdmi_aligner_merge_partial_window (f32 snippets) over all N frames: per frame
+    the sum over this rank's (dilation, local snippet, slot) of s·x + t, slots in the reference's
+    k-ascending order (w: snippet length per dilation); the window's rows are slices of it."""
     out = torch.zeros((N, HW), dtype=torch.float32)
     for f in range(N):
         acc = torch.zeros(HW, dtype=torch.float32)
@@ -54,8 +55,7 @@ def _worker(rank, world, port, res):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import rd_oracle as O
-    from rollingdepth_amd.shard import (_all_gather_rows, _all_reduce_minmax, _broadcast, _reduce_scatter_rows,
-                                        chunk_bounds, exchange_window_rows, frame_ranges, gather_rows_by_dilation,
+    from rollingdepth_amd.shard import (_all_gather_rows, _all_reduce_minmax, _broadcast, chunk_bounds, exchange_window_rows, frame_ranges, gather_rows_by_dilation,
                                         merge_exchange_plan, rank_subsets)
 
     ok = True
@@ -87,7 +87,9 @@ def _worker(rank, world, port, res):
     # --- global min / max -----------------------------------------------------------------------------
     mm = _all_reduce_minmax(torch.tensor([float(rank) - 5.0, 10.0 * rank]))
     ok &= mm.tolist() == [-5.0, 10.0 * (world - 1)]
-    # --- merge: rank-local sums, reduce-scatter by frame, ÷ cover count == merge_scaled_triplets -----
+    # --- windowed merge: sums over the rank's covered frame ranges only, all-to-all of the rows each
+    # chunk needs, pieces added per frame in source-rank order (rdmi_aligner_merge_finish_pieces),
+    # ÷ cover count == merge_scaled_triplets ------------------------------------------------------------
     N, H, W = 14, 4, 5
     w = [3, 2]  # snippet lengths per dilation
     dil = [1, 4]
@@ -100,17 +102,10 @@ def _worker(rank, world, port, res):
     k0 = [s[0] if s else 0 for s in sub]
     rows = [full[d][k0[d]:k0[d] + len(sub[d])] for d in range(len(dil))]
     sums = _merge_partial_cpu(rows, k0, n, dil, sc, tr, w, N, H * W)
-    mine = _reduce_scatter_rows(sums, world)
     f0, f1 = chunk_bounds(N, world)[rank]
-    merged_mine = torch.stack([mine[i] / _cover(n, dil, w, f0 + i) for i in range(f1 - f0)]) if f1 > f0 else mine
-    merged = _all_gather_rows(merged_mine, N, world)
     idx = [O.aligner_indices(N, d - 1, wd) for d, wd in zip(dil, w)]
     ref = O.aligner_merge([x.numpy()[:, :, None] for x in full], idx, [s.numpy() for s in sc],
                           [t.numpy() for t in tr], N)
-    err = np.abs(merged.numpy() - ref.reshape(N, H * W)).max()
-    ok &= bool(err < 1e-5)
-    # --- windowed merge (round 5): sums over the rank's covered frame ranges only, all-to-all of the rows
-    # each chunk needs, pieces added per frame in source-rank order (rdmi_aligner_merge_finish_pieces) --
     ranges, send, recv = merge_exchange_plan(n, dil, w, N, world, rank)
     ok &= ranges == frame_ranges(sub, dil, w)
     covered = {f for d in range(len(dil)) for k in sub[d] for j in range(w[d]) for f in [k + j * dil[d]]}

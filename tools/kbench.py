@@ -269,7 +269,10 @@ def bench_pair(iters):
 
 def bench_attn(iters):
     for lab, B, S, H in [("L0 S=27648 H=5 b=8", 8, 27648, 5), ("L1 S=6912 H=10 b=8", 8, 6912, 10),
-                         ("L2 S=1728 H=20 b=8", 8, 1728, 20), ("mid S=432 H=20 b=8", 8, 432, 20)]:
+                         ("L2 S=1728 H=20 b=8", 8, 1728, 20), ("mid S=432 H=20 b=8", 8, 432, 20),
+                         # the pipeline's launch shapes (25-snippet UNet batches)
+                         ("L0 S=27648 H=5 b=25", 25, 27648, 5), ("L1 S=6912 H=10 b=25", 25, 6912, 10),
+                         ("L2 S=1728 H=20 b=25", 25, 1728, 20)]:
         C = H * 64
         qkv = torch.randn(B, S, 3 * C, device="cuda").half()
         q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]

@@ -1,0 +1,18 @@
+# round 6 session c: PMC traffic passes (with launch sequence) + clock / MFMA-busy pass of one fast step
+cd /root/repo && mkdir -p gpurun_out && export TMPDIR=/tmp
+OUT=gpurun_out/r06c_pmc bash tools/pmc_bench.sh > gpurun_out/r06c_pmc.log 2>&1 || exit $?
+rm -rf gpurun_out/r06c_clk
+timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --output-format csv \
+  -d gpurun_out/r06c_clk -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-validate \
+  > gpurun_out/r06c_clk.log 2>&1 || exit $?
+python tools/pmc_clock.py gpurun_out/r06c_clk > gpurun_out/r06c_pmc_clock.txt
+python tools/traffic_split.py --fetch gpurun_out/r06c_pmc/FETCH_SIZE --write gpurun_out/r06c_pmc/WRITE_SIZE \
+  > gpurun_out/r06c_split_gemm.txt 2>&1
+python tools/traffic_split.py --fetch gpurun_out/r06c_pmc/FETCH_SIZE --write gpurun_out/r06c_pmc/WRITE_SIZE \
+  --family attention_fwd > gpurun_out/r06c_split_attn.txt 2>&1
+python tools/bench_traffic.py --fetch gpurun_out/r06c_pmc/FETCH_SIZE --write gpurun_out/r06c_pmc/WRITE_SIZE \
+  --preset fast --source "profiles/r06c_pmc_bench_fast.txt (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one fast step, round 6)" \
+  --summary gpurun_out/r06c_pmc_summary.txt --out gpurun_out/r06c_bench_traffic.json > gpurun_out/r06c_traffic.log 2>&1
+# raw per-dispatch CSVs are large: keep only what the summaries need
+find gpurun_out/r06c_pmc gpurun_out/r06c_clk -name '*.csv' -size +20M -delete
+echo done
