@@ -774,7 +774,7 @@ extern "C" int rdmi_aligner_merge_partial_window(int n_dil, const void* const* x
 extern "C" int rdmi_aligner_merge_finish_pieces(int n_dil, const int* n, const int* stride, const int* w, int f0,
                                                 int nf, long HW, int npieces, const int* piece_f0,
                                                 const int* piece_nf, const double* recv, float* out, void* stream) {
-  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && out && HW > 0 && f0 >= 0 && nf >= 0 &&
+  RDMI_REQUIRE(n_dil >= 1 && n_dil <= MAXD && n && stride && w && (out || nf == 0) && HW > 0 && f0 >= 0 && nf >= 0 &&
                    npieces >= 0 && (npieces == 0 || (piece_f0 && piece_nf && recv)),
                RDMI_E_ARG, "aligner_merge_finish_pieces: bad args");
   if (nf == 0) return 0;

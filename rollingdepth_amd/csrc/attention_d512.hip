@@ -53,8 +53,10 @@ __global__ __launch_bounds__(64 * NW5, 1) void attn_fwd_d512(Attn512P p) {
   const int wid = tid >> 6;
   const int hq = lane >> 4;   // lane quarter
   const int j16 = lane & 15;
-  int qblk, b, z_;
-  rdmi::xcd_block3(qblk, b, z_);  // (query block, image): one XCD streams one image's K / Vᵀ
+  // dispatch order (query block fastest): every XCD takes part in every image.  The XCD-local order of
+  // the d = 64 kernel (rdmi::xcd_block3: one image per XCD) measured 2-4 % slower here, bitwise equal
+  // (profiles/r06a_attn_xcd_ab.log; an image's 19 MB of K / Vᵀ exceeds one XCD's 4 MB L2 either way)
+  const int qblk = blockIdx.x, b = blockIdx.y;
   const int q = qblk * QB5 + wid * 16 + j16;
   // as the fix-up pass behind attn_fwd_d512_w4: only the 128-query blocks that pass flagged
   if (p.flags && p.flags[b * gridDim.x + qblk] == 0) return;
@@ -236,8 +238,7 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_d512_w4(Attn512P p) {
   const int wid = tid >> 6;
   const int hh = lane >> 5;
   const int j32 = lane & 31;
-  int qblk, b, z_;
-  rdmi::xcd_block3(qblk, b, z_);
+  const int qblk = blockIdx.x, b = blockIdx.y;
   const int q = qblk * 128 + wid * 32 + j32;
 
   const f16* Q = p.q + (long)b * p.q_bs;
