@@ -270,6 +270,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     p.group_m = gm ? atoi(gm) : 8;
     const char* cpp = getenv("RDMI_CONV_PIPE");
     p.conv_pipe = !cpp || cpp[0] != '0';
+    const char* hpf = getenv("RDMI_HALO_PREF");  // opt-in A/B: L2 prefetch of the next channel block's halo
+    p.halo_pref = hpf && hpf[0] == '1';
     const char* cp = getenv("RDMI_CPERM");
     p.cperm = (!cp || cp[0] != '0') && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 &&
               (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0));

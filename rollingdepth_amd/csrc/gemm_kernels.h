@@ -38,6 +38,7 @@ struct GemmP {
   const float* gaff;  // optional [B][Cin/64][2][64] scale / shift table (rdmi_conv_args.in_affine)
   int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
   int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
+  int halo_pref;   // conv_halo_occ2_kernel: L2 prefetch of the next channel block's halo (RDMI_HALO_PREF)
   unsigned long long* stamps;  // STAMP builds only (tools/conv_stamp.hip): per-wave segment cycle sums
 };
 
@@ -1432,7 +1433,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   constexpr int BSLOT = BN * BKP;          // halves (16 KiB)
   constexpr int NB = 4;                    // weight pieces per wave per K-tile (16 / 4 waves)
   constexpr int GNT = GN ? 256 : 0;        // sc[256], sh[256] floats (Cin <= 256)
-  __shared__ __attribute__((aligned(16))) f16 lds[HALO + 2 * BSLOT + 4 * GNT];
+  constexpr int PREF = 4 * 2 * 64 * 2;     // halves: the halo prefetch's landing area (4 waves × 2 × 64 dwords)
+  __shared__ __attribute__((aligned(16))) f16 lds[HALO + 2 * BSLOT + 4 * GNT + PREF];
   float* const gnt = (float*)(lds + HALO + 2 * BSLOT);
 
   const int tid = threadIdx.x;
@@ -1472,6 +1474,28 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
     hvo[e] = ok ? (unsigned)(((b * p.IH + sy) * p.IW + sx) * p.Cin + chunk * 8) * 2u : OOB;
   }
+  // Halo L2 prefetch (p.halo_pref, opt-in A/B): one dword of every 128-B line of the NEXT channel block's
+  // halo pieces this wave refills — lane l of instruction j covers pixel (j·64 + l) & 7 of piece
+  // wid + 4·((j·64 + l) >> 3) — loaded by LDS-DMA into a scratch area nothing reads, so that the refill's
+  // DMA finds the lines in L2 instead of HBM.  Arithmetic unchanged (bitwise the plain kernel).
+  unsigned pvo[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = j * 64 + lane, e = idx >> 3;
+    const int hp = (wid + 4 * e) * 8 + (idx & 7);
+    const int hr = hp / HWD, hc = hp - hr * HWD;
+    const int yy = y0 - 1 + pa + hr, xx = x0 - 1 + pc + hc;
+    const bool ok = e < HPW && wid + 4 * e < HPC && hp < HPIX && (unsigned)yy < (unsigned)Hl && (unsigned)xx < (unsigned)Wl;
+    const int sy = MODE == 2 ? yy >> 1 : yy, sx = MODE == 2 ? xx >> 1 : xx;
+    pvo[j] = ok ? (unsigned)(((b * p.IH + sy) * p.IW + sx) * p.Cin) * 2u : OOB;
+  }
+  auto prefetchHalo = [&](int cb) {
+    f16* lp = lds + HALO + 2 * BSLOT + 4 * GNT + wids * 256;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (__attribute__((address_space(3))) void*)(lp + j * 128), 4,
+                                               pvo[j], cb * 128, 0, 0);
+  };
   unsigned bvo[NB];  // weight DMA byte offsets of this lane's rows at K-tile 0 (the K step goes in soffset)
 #pragma unroll
   for (int e = 0; e < NB; ++e) {
@@ -1581,6 +1605,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     // MODE 3: K-tiles 0-3 the hi parts of taps t = 2dy + dx, 4-6 the lo parts of the taps t ≠ phase
     const int t4 = tap < 4 ? tap : tap - 4 + (tap - 4 >= phs ? 1 : 0);
     const int dy = MODE == 3 ? t4 >> 1 : (tap * 11) >> 5, dx = MODE == 3 ? t4 & 1 : tap - 3 * dy;
+    const bool pf = p.halo_pref && cb + 1 < ncb && NT > 2;  // wave-uniform
     if (u > 0) seg(2);
     if (u > 0) {
       if (tap == 0) {  // refill the halo with channel block cb
@@ -1592,7 +1617,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
         wait_vmcnt<0>();  // B(u) and the halo pieces of this wave (and its scale / shift loads)
         if constexpr (GN) xformHalo(cb);
       } else {
-        wait_vmcnt<0>();  // B(u), issued one K-tile ago
+        // B(u), issued one K-tile ago — and, at tap 2 with a prefetch in flight (issued after B(u) at
+        // tap 1), everything but the prefetch's two loads (loads complete in issue order)
+        if (pf && tap == 2)
+          wait_vmcnt<2>();
+        else
+          wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of B(u-1) done (slot reuse)
       }
       asm volatile("" ::: "memory");
@@ -1601,6 +1631,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
       if (tap == 0) seg(3); else seg(1);
     }
     if (u + 1 < nk) issueB(u + 1);
+    if (pf && tap == 1) prefetchHalo(cb + 1);
     const f16* lb = lds + HALO + (u & 1) * BSLOT + (wn * 64) * BKP;
     const int xb = fr + dx + 2 * dy;
     // A fragment (kh, i): halo row wms·RM + i + dy, pixel dx + fr, 16-B chunk (kh·4 + fq) ^ ((xb + 2i) & 7).

@@ -590,7 +590,9 @@ _ws_cache = {}
 
 
 def _workspace(n_floats: int, device) -> torch.Tensor:
-    key = (device, "ws")
+    # one scratch buffer per (device, stream): kernels queued on different streams (the pipeline's
+    # decode stream, RDMI_DECODE_STREAM) may run concurrently
+    key = (device, "ws", torch.cuda.current_stream().cuda_stream)
     t = _ws_cache.get(key)
     if t is None or t.numel() < n_floats:
         t = torch.empty(max(n_floats, 1 << 16), dtype=F32, device=device)

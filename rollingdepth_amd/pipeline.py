@@ -137,6 +137,12 @@ class RollingDepthPipeline:
         # directly, where it moves the whole map.  The returned snippet_ls keeps the
         # reference's dtype (the pipeline's).  RDMI_DEPTH_F32=0: f16 decoded depth.
         self.depth_f32 = os.environ.get("RDMI_DEPTH_F32", "1") == "1"
+        # Snippet decode on a second stream (RDMI_DECODE_STREAM=1, A/B): the VAE decode of UNet batch i runs
+        # beside the UNet of batch i + 1, so each kernel's last partial round of workgroups and the
+        # HBM-bound norm passes can share the chip with the other stream's kernels.  Every kernel computes
+        # the same values either way (no cross-stream reductions): bitwise the serial forward.
+        self.decode_stream = os.environ.get("RDMI_DECODE_STREAM", "0") == "1"
+        self._dstream = None
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -363,6 +369,11 @@ class RollingDepthPipeline:
             else:
                 groups.append((key, [(di, todo, fr)]))
         outs: List[Optional[torch.Tensor]] = [None] * len(dilations)
+        ds = None
+        if self.decode_stream and self.device.type == "cuda":
+            if self._dstream is None:
+                self._dstream = torch.cuda.Stream(self.device)
+            ds = self._dstream
         for (slen, steps), members in groups:
             self.scheduler.set_timesteps(steps)
             timesteps = self.scheduler.timesteps
@@ -399,8 +410,20 @@ class RollingDepthPipeline:
                         self.scheduler.step_(pred, int(t), depth_view, 1.0, channels=4, out=x2[..., 4:])
                         x = x2
                         depth_view = x[..., 4:8]
-                self.decode_depth(zin, buf[b0:b1].view(nb * slen, H, W, 1))
+                if ds is None:
+                    self.decode_depth(zin, buf[b0:b1].view(nb * slen, H, W, 1))
+                else:  # the decode waits for this batch's DDIM step; the next UNet batch does not wait for it
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    with torch.cuda.stream(ds):
+                        ds.wait_event(ev)
+                        self.decode_depth(zin, buf[b0:b1].view(nb * slen, H, W, 1))
+                    zin.record_stream(ds)
                 _progress(f"dilations {[dilations[m[0]] for m in members]}: snippets {b1}/{ntodo} decoded")
+        if ds is not None:  # the decoded snippets are read on the launch stream from here on
+            done = torch.cuda.Event()
+            done.record(ds)
+            torch.cuda.current_stream().wait_event(done)
         return outs
 
     def refine(self, rgb_latent: torch.Tensor, depth_latents: torch.Tensor, init_noise: torch.Tensor,

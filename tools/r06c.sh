@@ -1,5 +1,7 @@
 # round 6 session c: PMC traffic passes (with launch sequence) + clock / MFMA-busy pass of one fast step
 cd /root/repo && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 500 python -u tools/decode_stream_ab.py > gpurun_out/r06c_decode_stream_ab.log 2>&1; rc=$?; echo "decode stream exit $rc"
+case $rc in 124|134|137|139) exit $rc;; esac
 OUT=gpurun_out/r06c_pmc bash tools/pmc_bench.sh > gpurun_out/r06c_pmc.log 2>&1 || exit $?
 rm -rf gpurun_out/r06c_clk
 timeout -s KILL 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --output-format csv \
@@ -15,4 +17,11 @@ python tools/bench_traffic.py --fetch gpurun_out/r06c_pmc/FETCH_SIZE --write gpu
   --summary gpurun_out/r06c_pmc_summary.txt --out gpurun_out/r06c_bench_traffic.json > gpurun_out/r06c_traffic.log 2>&1
 # raw per-dispatch CSVs are large: keep only what the summaries need
 find gpurun_out/r06c_pmc gpurun_out/r06c_clk -name '*.csv' -size +20M -delete
-echo done
+echo done1
+# halo L2 prefetch (RDMI_HALO_PREF, opt-in): bits and interleaved kernel A/B
+timeout -k 10 300 python -u tools/conv_bits.py > gpurun_out/r06c_convbits_0.txt 2>&1 || exit $?
+RDMI_HALO_PREF=1 timeout -k 10 300 python -u tools/conv_bits.py > gpurun_out/r06c_convbits_1.txt 2>&1 || exit $?
+diff gpurun_out/r06c_convbits_0.txt gpurun_out/r06c_convbits_1.txt > /dev/null && echo "halo pref bits: equal" || echo "halo pref bits: DIFFER"
+timeout -k 10 600 python -u tools/env_ab.py --var RDMI_HALO_PREF --values 0,1 --bench conv --rounds 2 > gpurun_out/r06c_halo_pref_conv_ab.log 2>&1 || exit $?
+timeout -k 10 600 python -u tools/env_ab.py --var RDMI_HALO_PREF --values 0,1 --bench gnconv --rounds 2 > gpurun_out/r06c_halo_pref_gnconv_ab.log 2>&1 || exit $?
+echo done2

@@ -41,10 +41,14 @@ def main():
     ap.add_argument("--write", required=True)
     ap.add_argument("--family", default="implicit_gemm")
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--counters", default="FETCH_SIZE,WRITE_SIZE", help="passes to read (a FETCH-only run: FETCH_SIZE)")
     a = ap.parse_args()
     fams = [f for f, _ in FAMILIES]
     res = {}
+    want = a.counters.split(",")
     for d, cn, mul in ((a.fetch, "FETCH_SIZE", 2.0), (a.write, "WRITE_SIZE", 1.0)):
+        if cn not in want:
+            continue
         seq = json.load(open(os.path.join(d, "seq.json")))
         seq = [s for s in seq if s[0] == a.family]
         rows = [r for r in dispatches(d, cn) if family(r[1]) == a.family]
@@ -53,7 +57,7 @@ def main():
         for (_, kn, v), (_, shape, flop, nb) in zip(rows, seq):
             e = res.setdefault((short(kn), shape), {"n": 0, "alg": 0.0, "flop": 0.0, "FETCH_SIZE": 0.0,
                                                     "WRITE_SIZE": 0.0})
-            if cn == "FETCH_SIZE":
+            if cn == want[0]:
                 e["n"] += 1
                 e["alg"] += nb
                 e["flop"] += flop
