@@ -735,3 +735,26 @@ def test_resize_nearest(H, W, Ho, Wo):
     ref = F.interpolate(x.permute(0, 3, 1, 2).float(), size=(Ho, Wo), mode="nearest").half().permute(0, 2, 3, 1)
     assert torch.equal(y, ref)
 
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,up,gn", [(2, 32, 32, 128, 128, False, True), (1, 16, 32, 256, 256, False, True),
+                                                  (1, 16, 16, 512, 128, False, False), (1, 8, 16, 256, 128, True, False),
+                                                  (2, 16, 16, 64, 128, False, True)])
+def test_conv_halo_prefetch_bitwise(B, H, W, Cin, Cout, up, gn, monkeypatch):
+    """RDMI_HALO_PREF (the occ2 halo conv's L2 prefetch of the next channel block's halo) only adds loads
+    into a scratch LDS area: outputs bitwise equal with and without it (one channel block included)."""
+    K_ = _k()
+    g = torch.Generator(device=DEV).manual_seed(33)
+    x = torch.randn(B, H, W, Cin, device=DEV, generator=g).half()
+    wp = K_.pack_conv(torch.randn(Cout, Cin, 3, 3) / math.sqrt(Cin * 9), DEV)
+    bias = torch.randn(Cout, device=DEV, generator=g)
+    ig = None
+    if gn:
+        gm = 1 + 0.2 * torch.randn(Cin, device=DEV, generator=g)
+        bt = 0.2 * torch.randn(Cin, device=DEV, generator=g)
+        ig = (K_.groupnorm_stats(x, 32, 1e-6), gm, bt, 32, True)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RDMI_HALO_PREF", v)
+        outs.append(K_.conv2d(x, wp, Cout, 3, upsample=up, bias=bias, in_gn=ig))
+    assert torch.equal(outs[0], outs[1])

@@ -560,3 +560,23 @@ def test_sharded_forward_multi_rank_one_gpu(name, dtype_name, world, seeded):
     # per-launch-shape engine choices could separate the two — none at these sizes (measured: 0.0,
     # profiles/r04c_gpu_tests.log); bound at f16-rounding level
     assert res[0] <= 1e-5 and res[1] <= 1e-3 and res[2] == 0, list(res)
+
+
+def test_decode_stream_forward_bitwise():
+    """RDMI_DECODE_STREAM / pipe.decode_stream: each UNet batch's VAE decode on a second stream, beside the
+    next batch's UNet — every kernel computes the same values, so the forward is bitwise the serial one
+    (snippet batch 2 so that several decodes overlap UNet batches)."""
+    from rollingdepth_amd.pipeline import RollingDepthPipeline
+
+    t = load_file(os.path.join(G, "tiny_pipeline.safetensors"))
+    meta = json.load(open(os.path.join(G, "tiny_pipeline.json")))
+    pipe = RollingDepthPipeline.from_synthetic(meta["unet"], meta["vae"], meta["scheduler"], device="cuda")
+    pipe.snippet_batch = 2
+    pipe.empty_text_embed = t["context"]
+    res = []
+    for mode in (False, True):
+        pipe.decode_stream = mode
+        out = pipe.forward(t["frames"][None], list(meta["dilations_in"]), meta["cap_dilation"], [3], [1], [1],
+                           None, 0, 3, 6, None, False, 4, False, init_noise=t["init_noise"])
+        res.append((out.depth_pred.float(), torch.cat([s.float().reshape(-1) for s in out.snippet_ls])))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

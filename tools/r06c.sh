@@ -25,3 +25,6 @@ diff gpurun_out/r06c_convbits_0.txt gpurun_out/r06c_convbits_1.txt > /dev/null &
 timeout -k 10 600 python -u tools/env_ab.py --var RDMI_HALO_PREF --values 0,1 --bench conv --rounds 2 > gpurun_out/r06c_halo_pref_conv_ab.log 2>&1 || exit $?
 timeout -k 10 600 python -u tools/env_ab.py --var RDMI_HALO_PREF --values 0,1 --bench gnconv --rounds 2 > gpurun_out/r06c_halo_pref_gnconv_ab.log 2>&1 || exit $?
 echo done2
+timeout -k 10 600 python -u tools/gemm_k32_ab.py > gpurun_out/r06c_gemm_k32_ab.log 2>&1; echo "k32 exit $?"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_kernels_gpu.py \
+  tests/test_pipeline_gpu.py -k "k32 or prefetch or decode_stream" > gpurun_out/r06c_new_tests.log 2>&1; echo "new tests exit $?"
