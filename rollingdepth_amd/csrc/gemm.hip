@@ -156,7 +156,8 @@ bool halo_eligible(const rdmi_conv_args* a, int hmode) {
 // channels (≤ 256 in the two-workgroups-per-CU variant, the only one for Cout % 256 != 0 other than
 // 128); with in_affine (the table in global memory, read per channel block) any Cin — only
 // conv_halo_occ2_kernel reads that table, so rdmi_conv2d sends every in_affine conv to it whatever
-// RDMI_CONV_HALO selects (the 256-wide and 8-wave engines keep their fixed 1024-entry LDS table)
+// RDMI_CONV_HALO selects (the 256-wide and 8-wave engines keep their fixed 1024-entry LDS table); the
+// opt-in 32×32×16 engine takes GroupNorm only for Cin ≤ 256, from the LDS table it builds itself
 bool in_gn_ok(const rdmi_conv_args* a) {
   const int cmax = a->in_affine ? (1 << 30) : (a->Cout % 256 == 0 || a->Cout == 128) ? 1024 : 256;
   return a->in_groups > 0 && a->Cin <= cmax && a->Cin % a->in_groups == 0;
@@ -297,7 +298,7 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     } else if (a->Cout == 128 && !p.gaff && (hmode == 4 || (gn && a->Cin > 256))) {  // the 8-wave 128-channel variant
       dim3 g(1, patches, 1);
       launch_conv_halo(a->upsample ? 2 : 1, 1, 2, gn, g, st, p);
-    } else if (!p.gaff && h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches
+    } else if (h32_ok(a, p, gn)) {  // 32×32×16 MFMA form on 32×8 patches (GN: Cin ≤ 256, its own LDS table)
       dim3 g(a->Cout / 128, (unsigned)((a->Ho / 8) * (a->Wo / 32) * a->B), 1);
       launch_conv_h32(gn, g, st, p);
     } else {  // two workgroups per CU (RDMI_CONV_HALO=3: also for Cout % 256 == 0)

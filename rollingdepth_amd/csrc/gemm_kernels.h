@@ -1787,7 +1787,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   const int lrow = lane >> 3, pc = lane & 7;
   unsigned hoff[HPW];  // byte offset of this lane's 16 B of halo piece e in channel block 0, or OOB
   // logical chunk of this lane in piece e (GroupNorm channels 8·lc .. +8 of the block)
-  auto hlc = [&](int e) {
+  auto hlc = [&](int e) __attribute__((always_inline)) {
     const int hp = (wid + 4 * e) * 8 + lrow;
     return pc ^ (((hp - (hp / HC) * HC) >> 1) & 7);
   };
@@ -1809,14 +1809,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   }
   const int ncb = p.Cin >> 6;
   auto hv = [&](int e) { return wids + 4 * e < HPC; };
-  auto issueHalo = [&](int cb) {
+  auto issueHalo = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
     for (int e = 0; e < HPW; ++e)
       if (hv(e))
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ra_, (__attribute__((address_space(3))) void*)(lds + (wid + 4 * e) * 8 * BKP),
                                                  16, hoff[e], cb * 128, 0, 0);
   };
-  auto issueB = [&](int u) {
+  auto issueB = [&](int u) __attribute__((always_inline)) {
     f16* lb = lds + HALO + (u & 1) * BSLOT;
 #pragma unroll
     for (int e = 0; e < NB; ++e)
@@ -1826,11 +1826,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   unsigned inmask = 0;  // bit e: this lane's pixel of halo piece e lies inside the image
 #pragma unroll
   for (int e = 0; e < HPW; ++e) inmask |= (hoff[e] != OOB ? 1u : 0u) << e;
-  // in-place GroupNorm (+SiLU) of this wave's landed pieces: the instructions of
+  // in-place GroupNorm (+SiLU) of this wave's landed pieces (always_inline: called from every tap-0
+  // K-tile instantiation, hipcc otherwise outlined it and passed the captures through 464 B of scratch
+  // per lane — the 2.2× GroupNorm slowdown of round 5, profiles/r05b_h32_ab.log): the instructions of
   // conv_halo_occ2_kernel's transform (gn_xform_words: v_fma_mix affine, silu4, packed RNE
   // conversion, padding only in waves holding out-of-image pixels) — bitwise the unfused
   // gn_apply; the lane's logical chunk (and so its 8 scale / shift values) changes per piece here
-  auto xformHalo = [&](int cb) {
+  auto xformHalo = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
     for (int e = 0; e < HPW; ++e)
       if (hv(e)) {
@@ -1905,7 +1907,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
   asm volatile("" ::: "memory");
 
   // one K-tile: tap TAP of channel block cb, weights in slot PAR
-  auto ktile = [&](auto TAPc, auto PARc, int cb) {
+  auto ktile = [&](auto TAPc, auto PARc, int cb) __attribute__((always_inline)) {
     constexpr int TAP = decltype(TAPc)::value, PAR = decltype(PARc)::value;
     constexpr int dy = TAP / 3, dx = TAP % 3;
     const int u = cb * 9 + TAP;
@@ -1927,7 +1929,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
     }
     if (u + 1 < 9 * ncb) issueB(u + 1);
     f16x8 af[2][2], bf[2][4];
-    auto rd = [&](int ks, int buf) {
+    auto rd = [&](int ks, int buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         af[buf][c] = *(const f16x8*)LDS_PTR(f16, (uintptr_t)(woff[ks] + (PAR * BSLOT + c * 32 * BKP) * 2));
@@ -1947,7 +1949,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo32_kernel(GemmP p) {
     }
     h32_sched<4>();
   };
-  auto block = [&](auto PAR0, int cb) {  // the nine taps of channel block cb, slot parity alternating
+  auto block = [&](auto PAR0, int cb) __attribute__((always_inline)) {  // the nine taps of channel block cb, slot parity alternating
     constexpr int P0 = decltype(PAR0)::value;
     ktile(std::integral_constant<int, 0>{}, std::integral_constant<int, P0>{}, cb);
     ktile(std::integral_constant<int, 1>{}, std::integral_constant<int, P0 ^ 1>{}, cb);
