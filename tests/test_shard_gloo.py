@@ -1,4 +1,4 @@
-"""World-size-2 (and 3) gloo tests (CPU) of the multi-GPU plan of rollingdepth_amd/shard.py
+"""World-size-2, 3 and 8 gloo tests (CPU) of the multi-GPU plan of rollingdepth_amd/shard.py
 (SURVEY.md §8e).  The collectives and the rank/frame/snippet bookkeeping are the product's own
 functions; the per-rank device kernels (rdmi_aligner_merge_partial_window / rdmi_snippet_accumulate) are
 stood in for by a CPU restatement of their contract (the GPU tests check the kernels against the
@@ -241,3 +241,42 @@ def test_sharded_forward_honours_init_infer_steps_world2():
         p.join(180)
     assert all(p.exitcode == 0 for p in procs)
     assert list(res) == [1, 1]
+
+
+def test_shard_plan_world8():
+    """The plan at the driver's largest scaling point, W = 8: most ranks own 1-2 of the 14 merge frames
+    and of the 14 + 10 snippets, some none of a dilation, and chunk_bounds(11, 8) leaves the last
+    latent chunk empty."""
+    _run(8)
+
+
+def test_merge_exchange_plan_at_bench_shapes():
+    """The windowed merge's all-to-all plan (merge_exchange_plan) at the BASELINE configurations'
+    snippet counts for W = 2 … 24, planned independently on every rank: what rank s sends to rank r is
+    what r expects from s, every piece lies inside r's frame chunk and inside one of s's frame ranges,
+    and every frame a snippet slot of s covers reaches its owner from s."""
+    from rollingdepth_amd.shard import chunk_bounds, merge_exchange_plan, rank_subsets
+
+    cases = [(100, [1, 25], [3, 3]),        # configs[1] fast (and fast1024)
+             (100, [1, 10, 25], [3, 3, 3]),  # configs[3] full
+             (500, [1, 10, 25], [3, 3, 3]),  # configs[4] paper
+             (30, [1, 10], [3, 2])]          # mixed snippet lengths
+    for N, dil, w in cases:
+        counts = [N - (wd - 1) * d for d, wd in zip(dil, w)]
+        for W in (2, 4, 8, 24):
+            plans = [merge_exchange_plan(counts, dil, w, N, W, r) for r in range(W)]
+            chunks = chunk_bounds(N, W)
+            for s in range(W):
+                ranges, send, _ = plans[s]
+                assert sum(send) == sum(b - a for a, b in ranges)
+                sub = rank_subsets(counts, W, s)
+                slots = {k + j * dil[d] for d in range(len(dil)) for k in sub[d] for j in range(w[d])}
+                for r in range(W):
+                    pieces = plans[r][2][s]
+                    assert send[r] == sum(m for _, m in pieces)
+                    f0, f1 = chunks[r]
+                    for a, m in pieces:
+                        assert f0 <= a and a + m <= f1 and m > 0
+                        assert any(lo <= a and a + m <= hi for lo, hi in ranges)
+                    got = {f for a, m in pieces for f in range(a, a + m)}
+                    assert {f for f in slots if f0 <= f < f1} <= got
