@@ -1542,12 +1542,17 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
     }
     const float sc[8] = {aff[0][0], aff[0][1], aff[0][2], aff[0][3], aff[1][0], aff[1][1], aff[1][2], aff[1][3]};
     const float sh[8] = {aff[2][0], aff[2][1], aff[2][2], aff[2][3], aff[3][0], aff[3][1], aff[3][2], aff[3][3]};
+    // each piece's 16 B read one piece ahead of its arithmetic, so the read's LDS latency runs under the
+    // previous piece's transform instead of in front of it (same values, same writes: bitwise the
+    // read-then-transform loop).  Piece 0 (wid < 4 < HPC) exists in every wave.
+    unsigned wn[4];
+    *(f16x8*)wn = *(const f16x8*)(lds + wid * 8 * BKP + lane * 8);
 #pragma unroll
     for (int e = 0; e < HPW; ++e)
       if (hv(e)) {
         f16* lh = lds + (wid + 4 * e) * 8 * BKP + lane * 8;
-        unsigned w[4];
-        *(f16x8*)w = *(const f16x8*)lh;
+        unsigned w[4] = {wn[0], wn[1], wn[2], wn[3]};
+        if (e + 1 < HPW && hv(e + 1)) *(f16x8*)wn = *(const f16x8*)(lh + 4 * 8 * BKP);
         const bool in = hvo[e] != OOB;
         if (p.gsilu)  // the SiLU flag dispatched once per piece (see gn_elem)
           gn_xform_words<4, true>(w, sc, sh, in);

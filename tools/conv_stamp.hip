@@ -4,8 +4,11 @@
 // 128-channel shape: 768² 128 → 128, B images, GroupNorm+SiLU input, residual and GroupNorm moments
 // out (the VAE ResnetBlock2D conv2).  Read the SHARES, not the stamped build's run time.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/conv_stamp.hip -o tools/conv_stamp
-//   ./tools/conv_stamp [B] [HW] [gn res moments: 0/1 each] [Cin] [Cout] [residual row stride]
+//   ./tools/conv_stamp [B] [HW] [gn res moments: 0/1 each] [Cin] [Cout] [residual row stride] [gaff 0/1]
 // Cout = 128: conv_halo_occ2_kernel; Cout % 256 == 0: conv_halo_kernel<1, 2, 4, GN> (8 waves, ping-pong).
+// gaff = 1: the GroupNorm scale / shift from the per-(image, channel block) table in global memory
+// (rdmi_conv_args.in_affine, the pipeline's default), any Cout on conv_halo_occ2_kernel — the dispatch
+// rdmi_conv2d makes for every in_affine conv.
 #include "../rollingdepth_amd/csrc/gemm_kernels.h"
 
 #include <algorithm>
@@ -53,8 +56,9 @@ int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 8, HW = argc > 2 ? atoi(argv[2]) : 768;
   const bool gn = argc > 3 ? atoi(argv[3]) : 1, res = argc > 4 ? atoi(argv[4]) : 1, mom = argc > 5 ? atoi(argv[5]) : 1;
   const int Cin = argc > 6 ? atoi(argv[6]) : 128, Cout = argc > 7 ? atoi(argv[7]) : 128, Kp = 9 * Cin, G = 32;
-  const bool wide = Cout % 256 == 0;
   const int rld = argc > 8 ? atoi(argv[8]) : Cout;  // residual row stride (0: every row reads one cached row)
+  const bool gaff = gn && argc > 9 && atoi(argv[9]) != 0;
+  const bool wide = Cout % 256 == 0 && !gaff;
   const int WPG = wide ? 8 : 4;  // waves per workgroup
   const long M = (long)B * HW * HW;
   f16 *x, *w, *y, *r;
@@ -80,7 +84,14 @@ int main(int argc, char** argv) {
   p.a_bytes = (unsigned)(M * Cin * 2); p.w_bytes = (unsigned)((long)Cout * Kp * 2);
   p.group_m = 8; p.cperm = 1; p.conv_pipe = 1;
   if (gn) { p.gmr = gmr; p.ggam = gam; p.gbet = bet; p.gG = G; p.gsilu = 1; }
-  const dim3 g(wide ? Cout / 256 : 1, (unsigned)((HW / 16) * (HW / 16) * B), 1);
+  if (gaff) {  // [B][Cin/64][64 scales | 64 shifts]
+    float* tab;
+    const long nt = (long)B * (Cin / 64) * 128;
+    CK(hipMalloc(&tab, nt * 4));
+    hipLaunchKernelGGL(fill_f, dim3(64), dim3(256), 0, 0, tab, nt, 0.9f, 0.05f);
+    p.gaff = tab;
+  }
+  const dim3 g(wide ? Cout / 256 : (Cout + 127) / 128, (unsigned)((HW / 16) * (HW / 16) * B), 1);
   const long nw = (long)g.x * g.y * WPG;
   unsigned long long* st;
   CK(hipMalloc(&st, nw * 8 * 8));
@@ -88,8 +99,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   const double fl = 2.0 * M * Cout * Kp;
-  printf("conv 3x3 %d->%d %dx%d B=%d gn=%d res=%d moments=%d: %u workgroups, %.1f GFLOP\n", Cin, Cout, HW, HW, B, gn,
-         res, mom, g.y, fl / 1e9);
+  printf("conv 3x3 %d->%d %dx%d B=%d gn=%d%s res=%d moments=%d: %u workgroups, %.1f GFLOP\n", Cin, Cout, HW, HW, B,
+         gn, gaff ? " (in_affine table)" : "", res, mom, g.x * g.y, fl / 1e9);
   for (int variant = 0; variant < 2; ++variant) {
     float best = 1e30f;
     for (int rep = 0; rep < 8; ++rep) {
