@@ -567,16 +567,22 @@ def gn_conv2d(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, groups: 
               w: torch.Tensor, cout: int, k: int, **conv_kw) -> torch.Tensor:
     """conv2d(silu?(GroupNorm(x))): the norm fused into the conv's input path where the halo
     engine runs it and it pays, else groupnorm then conv2d (identical values either way).
-    Policy (RDMI_GN_FUSE; tools/kbench.py gnconv on MI355X): 1 (default) fuses for Cin ≤ 256 — the
-    768²/384² VAE convs, −4…16 % against apply + conv; wider inputs (any Cin since round 5, through
-    the scale / shift table) stay unfused: every 128-channel output tile normalises the same input
-    halo again (512 → 512 at 96²: +14 %, 320 → 640 at 48²: +8 %, profiles/r05e_gnconv_kbench.log), and
-    at the pipeline's 75-frame batches also where kbench's 24/48-frame cases broke even or won — the
-    fused 96² 320 → 320, 640 → 320 and 384² 512 → 256 convs cost 6 + 4 + 23 ms a step more than the
-    apply passes they saved (29 ms, profiles/r05n_shapes.log against r04au); 2 fuses wherever
+    Policy (RDMI_GN_FUSE): 1 (default) fuses where the conv has Cin ≤ 256 — the 768²/384² VAE convs,
+    −4…16 % against apply + conv (tools/kbench.py gnconv) — or Cout ≤ 384, i.e. at most three
+    128-channel output tiles normalise the same input halo: at the fast preset's own batch sizes, in
+    one process interleaved (tools/gn_fuse_probe.py, profiles/r06n_gn_fuse_probe.log) the UNet's 96²
+    320-output convs (Cin 320 / 640 / 960) −4…−6 % and the decoder's 384² 512 → 256 conv −8 %; with four
+    or more output tiles the repeated transform eats the saved pass (512 → 512 at 96² / 192²: ±0…+1 %,
+    1920 → 640 at 48²: +2…+5 %), so those stay unfused.  The isolated per-launch gains (≈20 ms a step
+    summed) do not carry over in full: the pipeline A/B gives −0.1 % of the step, 3 of 4 interleaved
+    rounds (tools/pipe_env_ab.py, profiles/r06o_gn_fuse_pipe_ab.log) — inside the pipeline the apply pass
+    and the conv after it run back to back on a tensor the previous kernel has just written, which the
+    probe does not reproduce.  RDMI_GN_FUSE=3: round 5's Cin ≤ 256-only rule (A/B); 2 fuses wherever
     supported; 0 never."""
     mode = os.environ.get("RDMI_GN_FUSE", "1")
-    if mode != "0" and (mode == "2" or x.shape[-1] <= 256) and conv2d_in_gn_supported(
+    cin = x.shape[-1]
+    want = {"0": False, "2": True, "3": cin <= 256}.get(mode, cin <= 256 or cout <= 384)
+    if want and conv2d_in_gn_supported(
             x, w, cout, k, groups, conv_kw.get("stride", 1), conv_kw.get("pad", 1), conv_kw.get("upsample", False),
             conv_kw.get("rowbias"), conv_kw.get("out_hw")):
         mr = groupnorm_stats(x, groups, eps)
