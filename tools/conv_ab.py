@@ -30,6 +30,8 @@ CASES = [
     ("vae 256->128 768^2 x4 gn", 4, 768, 256, 128, False, "gn"),
     ("vae 256->128 768^2 x8 full", 8, 768, 256, 128, False, "full"),
     ("vae 256 384^2 x8 full", 8, 384, 256, 256, False, "full"),
+    ("vae 256 384^2 x18 gn", 18, 384, 256, 256, False, "gn"),
+    ("vae 256 384^2 x18 full", 18, 384, 256, 256, False, "full"),
     ("vae 512 192^2 x8 plain", 8, 192, 512, 512, False, "plain"),
     ("vae up 256 384->768 x8", 8, 384, 256, 256, True, "plain"),
     ("vae up 512 192->384 x8", 8, 192, 512, 512, True, "plain"),
