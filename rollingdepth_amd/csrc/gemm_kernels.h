@@ -1443,9 +1443,18 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   const int wm = wid >> 1, wn = wid & 1;
   const int wids = __builtin_amdgcn_readfirstlane(wid);
   const int nbx = gridDim.x;
-  const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
   int mt_, nt_;
-  tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  if (p.group_m < 0 && nbx > 1 && 8 % nbx == 0 && gridDim.y % (8 / nbx) == 0) {
+    // n-tile per XCD (RDMI_GEMM_GROUP=-1, A/B): dispatch id d runs on XCD d % 8; XCD x computes only
+    // n-tile x % nbx (8 / nbx XCDs share one, taking every (8 / nbx)-th m-tile), so its L2 holds one
+    // n-tile's weights (1.2 MB for the 512-channel convs) instead of all of them.  Same tiles.
+    const int bid = blockIdx.y * nbx + blockIdx.x, xcd = bid & 7;
+    nt_ = xcd % nbx;
+    mt_ = (bid >> 3) * (8 / nbx) + xcd / nbx;
+  } else {
+    const int logical = xcd_remap(blockIdx.y * nbx + blockIdx.x, nbx * gridDim.y);
+    tile_mn(logical, nbx, gridDim.y, p.group_m, mt_, nt_);
+  }
   const int n0 = nt_ * BN;
   constexpr int NT = MODE == 3 ? 7 : 9;  // K-tiles (taps) per channel block
   // MODE 3: m-tile = (image, phase, 16×16 tile of the Ho/2 × Wo/2 phase grid)

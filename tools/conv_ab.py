@@ -33,6 +33,8 @@ CASES = [
     ("vae 256 384^2 x18 gn", 18, 384, 256, 256, False, "gn"),
     ("vae 256 384^2 x18 full", 18, 384, 256, 256, False, "full"),
     ("vae 512 192^2 x8 plain", 8, 192, 512, 512, False, "plain"),
+    ("vae 512 192^2 x37 plain", 37, 192, 512, 512, False, "plain"),
+    ("vae 512 96^2 x75 plain", 75, 96, 512, 512, False, "plain"),
     ("vae up 256 384->768 x8", 8, 384, 256, 256, True, "plain"),
     ("vae up 512 192->384 x8", 8, 192, 512, 512, True, "plain"),
     ("vae up 512 96->192 x8", 8, 96, 512, 512, True, "plain"),
