@@ -269,6 +269,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
   if (halo_eligible(a, hmode)) {
     const char* gm = getenv("RDMI_GEMM_GROUP");
     p.group_m = gm ? atoi(gm) : 8;
+    const char* nx = getenv("RDMI_CONV_NXCD");  // n-tile per XCD in the two-workgroups-per-CU engine (A/B)
+    if (nx && nx[0] == '1') p.group_m = -1;
     const char* cpp = getenv("RDMI_CONV_PIPE");
     p.conv_pipe = !cpp || cpp[0] != '0';
     const char* hpf = getenv("RDMI_HALO_PREF");  // opt-in A/B: L2 prefetch of the next channel block's halo

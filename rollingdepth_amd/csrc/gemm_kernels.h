@@ -1445,7 +1445,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   const int nbx = gridDim.x;
   int mt_, nt_;
   if (p.group_m < 0 && nbx > 1 && 8 % nbx == 0 && gridDim.y % (8 / nbx) == 0) {
-    // n-tile per XCD (RDMI_GEMM_GROUP=-1, A/B): dispatch id d runs on XCD d % 8; XCD x computes only
+    // n-tile per XCD (RDMI_CONV_NXCD=1, A/B): dispatch id d runs on XCD d % 8; XCD x computes only
     // n-tile x % nbx (8 / nbx XCDs share one, taking every (8 / nbx)-th m-tile), so its L2 holds one
     // n-tile's weights (1.2 MB for the 512-channel convs) instead of all of them.  Same tiles.
     const int bid = blockIdx.y * nbx + blockIdx.x, xcd = bid & 7;
