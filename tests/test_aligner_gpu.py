@@ -178,8 +178,9 @@ def test_aligner_merge_finish_many_pieces():
 @pytest.mark.parametrize("case", ["small", "mixed", "metric"])
 def test_aligner_fused_loop_bitwise(case, monkeypatch):
     """The two-launch iteration (aligner.hip snippet_grad_adam: per-snippet last-chunk Adam, deferred
-    loss history, turned into rows per block of 128 iterations) gives bitwise the scales,
-    translations, loss history and merged depth of the three-kernel loop (RDMI_ALIGNER_FUSED=0).
+    loss history, turned into rows per block of 128 iterations) and the persistent single launch
+    (aligner_persist_k: one workgroup per frame, one grid barrier per iteration) give bitwise the
+    scales, translations, loss history and merged depth of the three-kernel loop (RDMI_ALIGNER_FUSED=0).
     'metric': the fast preset's aligner shape (N = 100 frames, dilations [1, 25], P = 5 929
     subsampled pixels of a 768² frame), 300 iterations (three history blocks)."""
     from rollingdepth_amd.aligner import DepthAligner
@@ -195,17 +196,19 @@ def test_aligner_fused_loop_bitwise(case, monkeypatch):
         iters = 300
     xs = [torch.from_numpy(x).to(DEV) for x in snips]
     outs = {}
-    for coop in ("1", "0"):
+    for coop in ("2", "1", "0"):
         monkeypatch.setenv("RDMI_ALIGNER_FUSED", coop)
         al = DepthAligner(device=torch.device(DEV), num_iterations=iters)
         m, s, t, h = al.run(xs, list(dil))
         torch.cuda.synchronize()
         outs[coop] = (m.cpu(), [v.cpu() for v in s], [v.cpu() for v in t], h)
-    a, b = outs["1"], outs["0"]
-    assert torch.equal(a[0], b[0])
-    for d in range(len(dil)):
-        assert torch.equal(a[1][d], b[1][d]) and torch.equal(a[2][d], b[2][d])
-    assert a[3] == b[3]
+    b = outs["0"]
+    for coop in ("2", "1"):  # '2': the persistent single launch (it fits every case here)
+        a = outs[coop]
+        assert torch.equal(a[0], b[0]), coop
+        for d in range(len(dil)):
+            assert torch.equal(a[1][d], b[1][d]) and torch.equal(a[2][d], b[2][d]), coop
+        assert a[3] == b[3], coop
 
 
 def test_aligner_row_overflow_raises_index_error():
