@@ -968,20 +968,6 @@ __global__ void prepare_k(PrepP p) {
 // [1,10,25] at 2000 iterations would otherwise need 1.4 GB).
 constexpr int HBLK = 128;
 
-// Workspace (floats): 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v
-// (2·ntot each), the per-snippet arrival counters (ntot, padded to 8 B), the bias-correction table
-// ((iters + 1)·2 doubles); with a history, the
-// fused loop's per-iteration slots for min(iters, HBLK) iterations: loss partials (2·ntot·PS
-// doubles), chunk min/max (2·N·PS) and pre-update parameters (2·ntot).
-long ws_floats(int N, long P, int ntot, int iters, bool hist, int wmax) {
-  long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L) + 4L * (iters + 1);
-  // the persistent loop's partials (2 parities), barrier words and per-iteration history
-  f += 8L * ntot * wmax + 2 + (hist ? 6L * iters * N + 2L * iters * ntot : 0);
-  const long slots = iters < HBLK ? iters : HBLK;
-  if (hist) f += slots * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
-  return f + 64;
-}
-
 // RDMI_ALIGNER_FUSED (read per call: A/B and the bitwise tests): 0 the three-kernel loop, unset / 1 the
 // two-launch loop (default), 2 the persistent loop where aligner_persist_upt fits (opt-in: bitwise the
 // same results, 56 vs 52 ms per 2 000 iterations at the fast preset — DESIGN App. A)
@@ -989,6 +975,21 @@ int loop_mode() {
   const char* e = getenv("RDMI_ALIGNER_FUSED");
   return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
 }
+
+// Workspace (floats): 4 double arrays (ntot·PS each), fpart (N·PS·4 doubles), T, Td (N·P each), m, v
+// (2·ntot each), the per-snippet arrival counters (ntot, padded to 8 B), the bias-correction table
+// ((iters + 1)·2 doubles); with a history, the
+// fused loop's per-iteration slots for min(iters, HBLK) iterations: loss partials (2·ntot·PS
+// doubles), chunk min/max (2·N·PS) and pre-update parameters (2·ntot).
+long ws_floats(int N, long P, int ntot, int iters, bool hist, int wmax) {
+  long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L) + 4L * (iters + 1);
+  // the persistent loop (opt-in, loop_mode 2): partials (2 parities), barrier words, per-iteration history
+  if (loop_mode() == 2) f += 8L * ntot * wmax + 2 + (hist ? 6L * iters * N + 2L * iters * ntot : 0);
+  const long slots = iters < HBLK ? iters : HBLK;
+  if (hist) f += slots * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
+  return f + 64;
+}
+
 
 // pixels per thread of the persistent loop (0: it does not fit).  Its grid is one workgroup per frame,
 // all resident at once (one per CU at most is needed), ≤ PCM covering slots per frame, ≤ PMAXS snippets.
@@ -1079,19 +1080,21 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   if (rc) return rc;
   int wmax = 1;
   for (int d = 0; d < p.nd; ++d) wmax = p.w[d] > wmax ? p.w[d] : wmax;
+  const int mode = loop_mode();
   PerP q{};
   q.iters = a->iters;
   q.wmax = wmax;
   q.denom = denom;
   q.spin_limit = 1L << 22;
-  q.part = (double*)fw; fw += 8L * ntot * wmax;
-  q.bar = (unsigned*)fw; fw += 2;
-  if (p.hist) {
-    q.hl = (double*)fw; fw += 4L * a->iters * p.N;
-    q.hmm = fw; fw += 2L * a->iters * p.N;
-    q.hst = fw; fw += 2L * a->iters * ntot;
+  if (mode == 2) {  // the region ws_floats reserves for mode 2 only
+    q.part = (double*)fw; fw += 8L * ntot * wmax;
+    q.bar = (unsigned*)fw; fw += 2;
+    if (p.hist) {
+      q.hl = (double*)fw; fw += 4L * a->iters * p.N;
+      q.hmm = fw; fw += 2L * a->iters * p.N;
+      q.hst = fw; fw += 2L * a->iters * ntot;
+    }
   }
-  const int mode = loop_mode();
   const int upt = mode == 2 ? aligner_persist_upt(p, a->iters) : 0;
   if (upt) {
     hipLaunchKernelGGL(zero_f32, dim3(1), dim3(64), 0, st, (float*)q.bar, 2L);  // arrival counter, error flag
