@@ -23,6 +23,8 @@
 // gets no gradient).  With one length for all dilations the rows are disjoint and the loops below
 // reduce to the plain per-dilation, per-slot order.
 #pragma clang fp contract(off)
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -478,12 +480,11 @@ __global__ __launch_bounds__(256) void aligner_history(AlP p, double denom, cons
 // terms differently (per slot, then slots in order, instead of per pixel chunk), which changes an
 // f64 sum by ~1e-16 relative — below the f32 rounding of the gradient except with probability
 // ~1e-9 per value (tests/test_aligner_gpu.py::test_aligner_fused_loop_bitwise checks the results bitwise
-// against the two- and three-launch loops).  Measured (tools/aligner_ab.py, STAMP build): bitwise equal,
-// but 56 vs 52 ms per 2 000 iterations — per iteration ≈37k cycles of arithmetic (two IEEE f32 divisions
-// and ≈12 f64 operations per (pixel, slot), now on 100 CUs instead of spread over all 256) and ≈24k in
-// the arrival-counter barrier; a form that beats the two-launch loop needs several workgroups per frame
-// (a per-frame exchange of the L1 scale partials before the gradient pass) and an XCD-hierarchical
-// barrier.
+// against the two- and three-launch loops).  Measured (tools/aligner_ab.py, STAMP build): with one
+// workgroup per frame and 64-lane butterflies for the block sums, 56 vs 52 ms per 2 000 iterations — the
+// 14-double gradient sum alone was ≈20k cycles of cross-lane shuffles; with two workgroups per frame (each
+// the frame's means over all pixels, the gradient over half the pixel rounds) and the reduce-scatter sum
+// (psums16), 48.9 vs 52.4 ms.  Opt-in: the whole aligner is ≈1 % of a fast-preset step.
 constexpr int PT = 1024;      // threads per workgroup (one workgroup per frame)
 constexpr int PCM = 6;        // covering slots per frame held in registers (the fast preset: 3 + 3)
 constexpr int PMAXS = 1024;   // snippets (ntot) whose s, t, m, v live in LDS
@@ -524,6 +525,37 @@ __device__ __forceinline__ void psums(double (&v)[NV], double* sh /* [16 * NV + 
   __syncthreads();  // sh reusable
 }
 
+// Sums of 16 doubles over the 1024-thread block with a reduce-scatter butterfly: at lane offsets 32, 16, 8, 4
+// each lane keeps half of its values and adds the partner's copy of that half (8 + 4 + 2 + 1 shuffles instead of
+// 4 × 16), so lane 4i ends with value i's wave sum after two more levels; then the 16 wave sums in wave order.
+// Every thread gets the results.  (A fixed order: deterministic; the grouping differs from psums.)
+__device__ __forceinline__ void psums16(double (&v)[16], double* sh /* [16 * 16 + 16] */) {
+  const int lane = threadIdx.x & 63;
+  double a8[8], a4[4], a2[2], a1;
+  const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a8[i] = (b5 ? v[i + 8] : v[i]) + __shfl_xor(b5 ? v[i] : v[i + 8], 32, 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) a4[i] = (b4 ? a8[i + 4] : a8[i]) + __shfl_xor(b4 ? a8[i] : a8[i + 4], 16, 64);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) a2[i] = (b3 ? a4[i + 2] : a4[i]) + __shfl_xor(b3 ? a4[i] : a4[i + 2], 8, 64);
+  a1 = (b2 ? a2[1] : a2[0]) + __shfl_xor(b2 ? a2[0] : a2[1], 4, 64);
+  a1 += __shfl_xor(a1, 2, 64);
+  a1 += __shfl_xor(a1, 1, 64);
+  const int w = threadIdx.x >> 6;
+  if ((lane & 3) == 0) sh[w * 16 + (lane >> 2)] = a1;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    double r = 0.0;
+    for (int k = 0; k < PT / 64; ++k) r += sh[k * 16 + threadIdx.x];
+    sh[(PT / 64) * 16 + threadIdx.x] = r;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = sh[(PT / 64) * 16 + i];
+  __syncthreads();  // sh reusable
+}
+
 // Grid barrier of iteration `it` (all N workgroups arrive once per iteration on one monotonic counter).
 // Thread 0's agent-scope partial stores are complete (vmcnt) before it arrives, as in snippet_grad_adam.
 __device__ __forceinline__ bool pbarrier(const PerP& q, unsigned target) {
@@ -558,9 +590,43 @@ __device__ __forceinline__ unsigned long long al_stamp() {
 }
 
 // STAMP = 1 (diagnostic, RDMI_ALIGNER_STAMPS=1): workgroup 0 prints its cycle sums per segment.
-template <int UPT, int STAMP = 0>
+// snippet_grad's per-(pixel, slot) terms over the pixel rounds [U0, U1) of the persistent loop
+template <int U0, int U1, int UPT>
+__device__ __forceinline__ void persist_grad(const AlP& p, const float (&xv)[PCM][UPT], const float (&T)[UPT],
+                                             const float (&Td)[UPT], const float* se, const float* te, int cnt,
+                                             float isc, float iscd, long P, int tid, double (&g)[16]) {
+#pragma unroll
+  for (int e = 0; e < PCM; ++e) {
+    if (e < cnt) {
+#pragma unroll
+      for (int u = U0; u < U1; ++u) {
+        if (tid + (long)u * PT < P) {
+          const float xvv = xv[e][u];
+          float a = addrn(mulrn(xvv, se[e]), te[e]);
+          float z = a - T[u];
+          float ac = fmaxf(a, 1e-3f);
+          float ad = 1.0f / ac;
+          float zd = ad - Td[u];
+          float g1 = (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) * isc;
+          float g2 = 0.f;
+          if (a >= 1e-3f) g2 = (zd > 0.f ? 1.f : (zd < 0.f ? -1.f : 0.f)) * iscd * (-1.0f / (ac * ac));
+          double gg = (double)g1 + (double)p.dw * (double)g2;
+          g[2 * e] += gg * (double)xvv;
+          g[2 * e + 1] += gg;
+          g[2 * PCM] += fabs((double)z) * (double)isc;
+          g[2 * PCM + 1] += fabs((double)zd) * (double)iscd;
+        }
+      }
+    }
+  }
+}
+
+// H workgroups per frame (blockIdx.y = hh): each computes the frame's means and scales over all its
+// pixels (cheap) and the gradient partials of its 1/H of the pixel rounds (the costly part).
+template <int UPT, int H, int STAMP = 0>
 __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
-  const int f = blockIdx.x, tid = threadIdx.x;
+  const int f = blockIdx.x, hh = blockIdx.y, tid = threadIdx.x;
+  static_assert(UPT % H == 0, "pixel rounds split evenly");
   unsigned long long st[5] = {}, tp = 0;
   auto seg = [&](int i) __attribute__((always_inline)) {
     if constexpr (STAMP) {
@@ -573,7 +639,7 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
   __shared__ float prm[2 * PMAXS], am[2 * PMAXS], av[2 * PMAXS];
   __shared__ int egk[PCM], ej[PCM], ecnt;
   __shared__ const float* ex[PCM];
-  __shared__ double sh[(PT / 64 + 1) * (2 * PCM + 2)];
+  __shared__ double sh[(PT / 64 + 1) * 16];
   __shared__ float rmm[2][PT / 64];
   // parameters (global snippet order: s then t), Adam moments zero (torch.optim.Adam's initial state)
   for (int i = tid; i < np; i += PT) {
@@ -664,46 +730,31 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
     const float scf = (float)(v2[0] / (double)P), scdf = (float)(v2[1] / (double)P);
     const float isc = 1.0f / scf, iscd = 1.0f / scdf;
     // ---- snippet_grad: per covering slot Σ g·x, Σ g; the frame's loss partials
-    double g[2 * PCM + 2];
+    double g[16];  // 2 per covering slot, the two loss partials at 2·PCM, 2·PCM + 1 (PCM ≤ 7), padding
+    static_assert(2 * PCM + 2 <= 16, "psums16 holds 16 values");
 #pragma unroll
-    for (int i = 0; i < 2 * PCM + 2; ++i) g[i] = 0.0;
-#pragma unroll
-    for (int e = 0; e < PCM; ++e) {
-      if (e < cnt) {
-#pragma unroll
-        for (int u = 0; u < UPT; ++u) {
-          if (tid + (long)u * PT < P) {
-            const float xvv = xv[e][u];
-            float a = addrn(mulrn(xvv, se[e]), te[e]);
-            float z = a - T[u];
-            float ac = fmaxf(a, 1e-3f);
-            float ad = 1.0f / ac;
-            float zd = ad - Td[u];
-            float g1 = (z > 0.f ? 1.f : (z < 0.f ? -1.f : 0.f)) * isc;
-            float g2 = 0.f;
-            if (a >= 1e-3f) g2 = (zd > 0.f ? 1.f : (zd < 0.f ? -1.f : 0.f)) * iscd * (-1.0f / (ac * ac));
-            double gg = (double)g1 + (double)p.dw * (double)g2;
-            g[2 * e] += gg * (double)xvv;
-            g[2 * e + 1] += gg;
-            g[2 * PCM] += fabs((double)z) * (double)isc;
-            g[2 * PCM + 1] += fabs((double)zd) * (double)iscd;
-          }
-        }
-      }
-    }
-    psums<2 * PCM + 2>(g, sh);
+    for (int i = 0; i < 16; ++i) g[i] = 0.0;
+    // the pixel rounds [U0, U1) of this workgroup: a uniform branch between compile-time ranges (a per-round
+    // predicate was if-converted by the compiler, every workgroup then computing every round)
+    if (H == 1)
+      persist_grad<0, UPT>(p, xv, T, Td, se, te, cnt, isc, iscd, P, tid, g);
+    else if (hh == 0)
+      persist_grad<0, UPT / H>(p, xv, T, Td, se, te, cnt, isc, iscd, P, tid, g);
+    else
+      persist_grad<UPT / H, UPT>(p, xv, T, Td, se, te, cnt, isc, iscd, P, tid, g);
+    psums16(g, sh);
     seg(1);
     if (tid == 0) {
-      double* pb = q.part + (long)buf * ntot * q.wmax * 2;
+      double* pb = q.part + (long)buf * ntot * q.wmax * H * 2;
       for (int e = 0; e < cnt; ++e) {
-        double* o = pb + ((long)egk[e] * q.wmax + ej[e]) * 2;
+        double* o = pb + (((long)egk[e] * q.wmax + ej[e]) * H + hh) * 2;
         __hip_atomic_store(o, g[2 * e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(o + 1, g[2 * e + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (q.hl) {
         const long h = (long)(it - 1) * p.N + f;
-        q.hl[2 * h] = g[2 * PCM];
-        q.hl[2 * h + 1] = g[2 * PCM + 1];
+        q.hl[2 * (h * H + hh)] = g[2 * PCM];
+        q.hl[2 * (h * H + hh) + 1] = g[2 * PCM + 1];
         float lo = rmm[0][0], hi = rmm[1][0];
         for (int w = 1; w < PT / 64; ++w) {
           lo = fminf(lo, rmm[0][w]);
@@ -714,8 +765,8 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
       }
     }
     seg(2);
-    if (!pbarrier(q, (unsigned)it * gridDim.x)) {  // not co-resident / timed out: fail loudly (NaN s, t)
-      if (f == 0)
+    if (!pbarrier(q, (unsigned)it * gridDim.x * gridDim.y)) {  // not co-resident / timed out: fail loudly (NaN s, t)
+      if (f == 0 && hh == 0)
         for (int i = tid; i < np; i += PT) {
           const int gk = i < ntot ? i : i - ntot;
           int d = 0;
@@ -729,7 +780,7 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
     const double bc1 = p.bct[2 * it], bc2 = p.bct[2 * it + 1];
     const float step_size = (float)(p.lr / bc1);
     const float bc2s = (float)sqrt(bc2);
-    const double* pb = q.part + (long)buf * ntot * q.wmax * 2;
+    const double* pb = q.part + (long)buf * ntot * q.wmax * H * 2;
     for (int i = tid; i < np; i += PT) {
       const bool is_t = i >= ntot;
       const int gk = is_t ? i - ntot : i;
@@ -740,8 +791,10 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
       for (int j = 0; j < p.w[d]; ++j) {
         int kk = 0;
         if (row_owner(p, p.rb[d] + j, k + j * p.stride[d], kk) != d) continue;  // overwritten slot: no term
-        gsum += __hip_atomic_load(pb + ((long)gk * q.wmax + j) * 2 + (is_t ? 1 : 0), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int h2 = 0; h2 < H; ++h2)
+          gsum += __hip_atomic_load(pb + (((long)gk * q.wmax + j) * H + h2) * 2 + (is_t ? 1 : 0), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
       }
       const float pv = prm[i];
       float gf = (float)(gsum * (double)gscale);
@@ -760,18 +813,18 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
       prm[i] = addrn(pv, mulrn(-step_size, m) / den);
       am[i] = m;
       av[i] = v;
-      if (q.hst && f == 0) q.hst[(long)(it - 1) * np + i] = pv;
+      if (q.hst && f == 0 && hh == 0) q.hst[(long)(it - 1) * np + i] = pv;
     }
     __syncthreads();
     seg(4);
   }
   if constexpr (STAMP) {
-    if ((f == 0 || f == gridDim.x - 1) && tid == 0)
+    if ((f == 0 || f == gridDim.x / 2) && hh == 0 && tid == 0)
       printf("aligner_persist wg %d cycles per iteration: stats %.0f grad %.0f publish %.0f barrier %.0f adam %.0f\n", f,
              (double)st[0] / q.iters, (double)st[1] / q.iters, (double)st[2] / q.iters, (double)st[3] / q.iters,
              (double)st[4] / q.iters);
   }
-  if (f == 0)
+  if (f == 0 && hh == 0)
     for (int i = tid; i < np; i += PT) {
       const int gk = i < ntot ? i : i - ntot;
       int d = 0;
@@ -783,14 +836,14 @@ __global__ __launch_bounds__(PT, 1) void aligner_persist_k(AlP p, PerP q) {
 // History rows of the persistent loop: iteration it0 + blockIdx.x from its per-frame partials (hist_row
 // with the loss summed over frames instead of over (snippet, pixel chunk) partials)
 __global__ __launch_bounds__(256) void aligner_history_frames(AlP p, double denom, const double* hl, const float* hmm,
-                                                              const float* hst) {
+                                                              const float* hst, int H) {
   const int it = 1 + blockIdx.x;
   const long h0 = (long)(it - 1) * p.N;
   __shared__ double sh[8];
   double L1 = 0.0, L2 = 0.0, soft = 0.0;
-  for (int i = threadIdx.x; i < p.N; i += 256) {
-    L1 += hl[2 * (h0 + i)];
-    L2 += hl[2 * (h0 + i) + 1];
+  for (int i = threadIdx.x; i < p.N * H; i += 256) {
+    L1 += hl[2 * (h0 * H + i)];
+    L2 += hl[2 * (h0 * H + i) + 1];
   }
   L1 = block_sum_d<256>(L1, sh);
   L2 = block_sum_d<256>(L2, sh);
@@ -970,7 +1023,7 @@ constexpr int HBLK = 128;
 
 // RDMI_ALIGNER_FUSED (read per call: A/B and the bitwise tests): 0 the three-kernel loop, unset / 1 the
 // two-launch loop (default), 2 the persistent loop where aligner_persist_upt fits (opt-in: bitwise the
-// same results, 56 vs 52 ms per 2 000 iterations at the fast preset — DESIGN App. A)
+// same results, 48.9 vs 52.4 ms per 2 000 iterations at the fast preset — DESIGN App. A)
 int loop_mode() {
   const char* e = getenv("RDMI_ALIGNER_FUSED");
   return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
@@ -984,7 +1037,7 @@ int loop_mode() {
 long ws_floats(int N, long P, int ntot, int iters, bool hist, int wmax) {
   long f = 8L * ntot * PS + 8L * N * PS + 2L * N * P + 4L * ntot + ((ntot + 1) & ~1L) + 4L * (iters + 1);
   // the persistent loop (opt-in, loop_mode 2): partials (2 parities), barrier words, per-iteration history
-  if (loop_mode() == 2) f += 8L * ntot * wmax + 2 + (hist ? 6L * iters * N + 2L * iters * ntot : 0);
+  if (loop_mode() == 2) f += 16L * ntot * wmax + 2 + (hist ? 10L * iters * N + 2L * iters * ntot : 0);  // H <= 2
   const long slots = iters < HBLK ? iters : HBLK;
   if (hist) f += slots * (4L * ntot * PS + 2L * N * PS + 2L * ntot) + 2;
   return f + 64;
@@ -1087,10 +1140,10 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   q.denom = denom;
   q.spin_limit = 1L << 22;
   if (mode == 2) {  // the region ws_floats reserves for mode 2 only
-    q.part = (double*)fw; fw += 8L * ntot * wmax;
+    q.part = (double*)fw; fw += 16L * ntot * wmax;
     q.bar = (unsigned*)fw; fw += 2;
     if (p.hist) {
-      q.hl = (double*)fw; fw += 4L * a->iters * p.N;
+      q.hl = (double*)fw; fw += 8L * a->iters * p.N;
       q.hmm = fw; fw += 2L * a->iters * p.N;
       q.hst = fw; fw += 2L * a->iters * ntot;
     }
@@ -1098,19 +1151,36 @@ extern "C" int rdmi_aligner_optimize(const rdmi_aligner_args* a, void* stream) {
   const int upt = mode == 2 ? aligner_persist_upt(p, a->iters) : 0;
   if (upt) {
     hipLaunchKernelGGL(zero_f32, dim3(1), dim3(64), 0, st, (float*)q.bar, 2L);  // arrival counter, error flag
-    if (upt == 2)
-      hipLaunchKernelGGL(aligner_persist_k<2>, dim3(p.N), dim3(PT), 0, st, p, q);
-    else if (upt == 4)
-      hipLaunchKernelGGL(aligner_persist_k<4>, dim3(p.N), dim3(PT), 0, st, p, q);
-    else if (getenv("RDMI_ALIGNER_STAMPS"))
-      hipLaunchKernelGGL((aligner_persist_k<6, 1>), dim3(p.N), dim3(PT), 0, st, p, q);
-    else
-      hipLaunchKernelGGL(aligner_persist_k<6>, dim3(p.N), dim3(PT), 0, st, p, q);
+    int cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int H = (upt % 2 == 0 && 2 * p.N <= cus && !getenv("RDMI_ALIGNER_PERSIST_H1")) ? 2 : 1;
+    const dim3 g(p.N, H);
+    const bool stamps = getenv("RDMI_ALIGNER_STAMPS") != nullptr;
+    if (H == 2) {
+      if (upt == 2)
+        hipLaunchKernelGGL((aligner_persist_k<2, 2>), g, dim3(PT), 0, st, p, q);
+      else if (upt == 4)
+        hipLaunchKernelGGL((aligner_persist_k<4, 2>), g, dim3(PT), 0, st, p, q);
+      else if (stamps)
+        hipLaunchKernelGGL((aligner_persist_k<6, 2, 1>), g, dim3(PT), 0, st, p, q);
+      else
+        hipLaunchKernelGGL((aligner_persist_k<6, 2>), g, dim3(PT), 0, st, p, q);
+    } else {
+      if (upt == 2)
+        hipLaunchKernelGGL((aligner_persist_k<2, 1>), g, dim3(PT), 0, st, p, q);
+      else if (upt == 4)
+        hipLaunchKernelGGL((aligner_persist_k<4, 1>), g, dim3(PT), 0, st, p, q);
+      else if (stamps)
+        hipLaunchKernelGGL((aligner_persist_k<6, 1, 1>), g, dim3(PT), 0, st, p, q);
+      else
+        hipLaunchKernelGGL((aligner_persist_k<6, 1>), g, dim3(PT), 0, st, p, q);
+    }
     rc = rdmi::check_launch("aligner_persist");
     if (rc) return rc;
     if (p.hist) {
       hipLaunchKernelGGL(aligner_history_frames, dim3(a->iters), dim3(256), 0, st, p, denom, (const double*)q.hl,
-                         (const float*)q.hmm, (const float*)q.hst);
+                         (const float*)q.hmm, (const float*)q.hst, H);
       return rdmi::check_launch("aligner_history");
     }
     return 0;
