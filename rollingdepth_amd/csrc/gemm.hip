@@ -275,6 +275,11 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     p.conv_pipe = !cpp || cpp[0] != '0';
     const char* hpf = getenv("RDMI_HALO_PREF");  // opt-in A/B: L2 prefetch of the next channel block's halo
     p.halo_pref = hpf && hpf[0] == '1';
+    // the GroupNorm halo transform at s_setprio 2 (its refill is the workgroup's critical path; the partner's
+    // MFMA issue waits): bitwise the same, pipeline −0.3 % in 5 of 5 interleaved rounds
+    // (profiles/r06zc_xprio_pipe_ab.log); RDMI_XFORM_PRIO=0 restores the flat priority (A/B)
+    const char* xp = getenv("RDMI_XFORM_PRIO");
+    p.xprio = !(xp && xp[0] == '0');
     const char* cp = getenv("RDMI_CPERM");
     p.cperm = (!cp || cp[0] != '0') && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 &&
               (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0));

@@ -39,6 +39,7 @@ struct GemmP {
   int cperm;       // halo convs: 32-channel output permutation for 16-B epilogue accesses (RDMI_CPERM)
   int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
   int halo_pref;   // conv_halo_occ2_kernel: L2 prefetch of the next channel block's halo (RDMI_HALO_PREF)
+  int xprio;       // conv_halo_occ2_kernel: the GroupNorm halo transform at s_setprio 2 (default; RDMI_XFORM_PRIO=0 off)
   unsigned long long* stamps;  // STAMP builds only (tools/conv_stamp.hip): per-wave segment cycle sums
 };
 
@@ -1605,7 +1606,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr (GN) {
+    if (p.xprio) __builtin_amdgcn_s_setprio(2);
     xformHalo(0);
+    if (p.xprio) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("" ::: "memory");
@@ -1629,7 +1632,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
         issueHalo(cb);
         if constexpr (GN) loadAff(cb);
         wait_vmcnt<0>();  // B(u) and the halo pieces of this wave (and its scale / shift loads)
-        if constexpr (GN) xformHalo(cb);
+        if constexpr (GN) {
+          if (p.xprio) __builtin_amdgcn_s_setprio(2);
+          xformHalo(cb);
+          if (p.xprio) __builtin_amdgcn_s_setprio(0);
+        }
       } else {
         // B(u), issued one K-tile ago — and, at tap 2 with a prefetch in flight (issued after B(u) at
         // tap 1), everything but the prefetch's two loads (loads complete in issue order)
