@@ -28,6 +28,7 @@ struct AttnP {
   long q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs;
   float sl2;  // scale * log2(e)
   unsigned long long* stamps;  // STAMP builds only (tools/attn_stamp.hip): per-wave segment cycle sums
+  int sprio;                   // attn_fwd_d64: the softmax block at s_setprio 2 (RDMI_ATTN_SPRIO, A/B)
 };
 
 // In-kernel stamp (diagnostic builds, STAMP = 1; guide §7 'In-kernel stamps'): s_memtime with the
@@ -266,6 +267,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
     asm volatile("" ::: "memory");
     seg(1);
     // ================= S(kt): softmax → P(kt); wait DMA(kt+2)
+    if (p.sprio) __builtin_amdgcn_s_setprio(2);
     issue(kt + 3);  // past the end: zero rows into a drained slot
     // ---- mask (last tile only; lane owns query c, keys (r&3)+8(r>>2)+4hh of each block)
     const int kbase = kt * KB;
@@ -321,6 +323,7 @@ __global__ __launch_bounds__(64 * NWV, 1) void attn_fwd_d64(AttnP p) {
       if (F16SUM) rs = psum();
     }
     l += rs;
+    if (p.sprio) __builtin_amdgcn_s_setprio(0);
     seg(2);
     attn_wait_vmcnt<2 * DPW>();  // DMA(kt+2) landed (DMA(kt+3) in flight)
     asm volatile("" ::: "memory");
@@ -1052,6 +1055,8 @@ extern "C" int rdmi_attention_fwd(const void* q, const void* k, const void* v, v
                RDMI_E_ALIGN, "attention_fwd: strides/pointers must be 16-byte aligned");
   AttnP p{(const f16*)q, (const f16*)k, (const f16*)v, (f16*)o, H, Sq, Sk, q_ld, k_ld, v_ld, o_ld, q_bs, k_bs, v_bs, o_bs,
           scale * 1.4426950408889634f, nullptr};
+  const char* sp = getenv("RDMI_ATTN_SPRIO");  // read per launch (A/B)
+  p.sprio = sp && sp[0] == '1';
   dim3 g(rdmi::div_up(Sq, QB), H, B);
   static const bool f32sum = [] { const char* e = getenv("RDMI_ATTN_F32SUM"); return e && e[0] == '1'; }();
   const char* pe = getenv("RDMI_ATTN_PIPE");  // read per launch (A/B): 1 = the one-wave-per-SIMD pipeline
