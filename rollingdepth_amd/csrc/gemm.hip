@@ -280,6 +280,8 @@ extern "C" int rdmi_conv2d(const rdmi_conv_args* a, void* stream) {
     // (profiles/r06zc_xprio_pipe_ab.log); RDMI_XFORM_PRIO=0 restores the flat priority (A/B)
     const char* xp = getenv("RDMI_XFORM_PRIO");
     p.xprio = !(xp && xp[0] == '0');
+    const char* ep = getenv("RDMI_EPI_PRIO");  // opt-in A/B: the halo conv's epilogue at s_setprio 2
+    p.eprio = ep && ep[0] == '1';
     const char* cp = getenv("RDMI_CPERM");
     p.cperm = (!cp || cp[0] != '0') && p.vec && ((uintptr_t)p.C & 15) == 0 && p.ldc % 8 == 0 &&
               (!p.R || (((uintptr_t)p.R & 15) == 0 && p.ldr % 8 == 0));

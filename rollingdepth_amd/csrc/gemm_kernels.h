@@ -40,6 +40,7 @@ struct GemmP {
   int conv_pipe;   // halo convs: software-pipelined fragment reads (RDMI_CONV_PIPE=0: all reads first, A/B)
   int halo_pref;   // conv_halo_occ2_kernel: L2 prefetch of the next channel block's halo (RDMI_HALO_PREF)
   int xprio;       // conv_halo_occ2_kernel: the GroupNorm halo transform at s_setprio 2 (default; RDMI_XFORM_PRIO=0 off)
+  int eprio;       // conv_halo_occ2_kernel: the epilogue at s_setprio 2 (RDMI_EPI_PRIO=1, A/B)
   unsigned long long* stamps;  // STAMP builds only (tools/conv_stamp.hip): per-wave segment cycle sums
 };
 
@@ -1718,6 +1719,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_occ2_kernel(GemmP p) {
   }
   seg(2);
   if (live) {
+    if (p.eprio) __builtin_amdgcn_s_setprio(2);  // RDMI_EPI_PRIO (A/B): the epilogue above the partner's MFMAs
     if constexpr (MODE == 3)
       store_tile<RM, RN, 64, true>(p, acc, PhaseRows{b, p.Ho, p.Wo, y0, x0, wm * RM, fr, pa, pc}, n0 + wn * 64, 0, fr,
                                    fq, p.cperm);
